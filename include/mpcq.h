@@ -1,0 +1,156 @@
+/*
+ * mpcq.h — C ABI of the MI355X-native batched convex-MPC QP engine (libmpcq.so).
+ *
+ * Drop-in boundary for the hot path of thomascbrs/mpc-tsid: the QP formulation
+ * in MPC.py and its OSQP solve.  Every entry point below names the reference
+ * interface it replaces (file:line in the reference tree).  Plain C types only:
+ * pointers + sizes, no torch / HIP types in the signatures.
+ *
+ * Problem (per instance, horizon N, MPC.py:98-288):
+ *   x = [X_1..X_N (12 each), f_0..f_{N-1} (12 each)]     n = 24N variables
+ *   rows: 12N dynamics | 12N swing mask | 20N friction    m = 44N constraints
+ *   min 1/2 x'Px   s.t.  l <= A x <= u     (P diagonal, q = 0)
+ * A is CSC with the fixed sparsity pattern of MPC.create_ML (nnz = 126N-18).
+ *
+ * Layouts (all C-order / row-major, float64):
+ *   xref    [B][12][N+1]   column 0 = current state (MPC.py:466-467)
+ *   fsteps  [B][20][13]    col 0 = phase duration, then foot xyz (NaN = swing)
+ *   Ax      [B][nnz]       CSC data, pattern from mpcq_pattern()
+ *   l, u    [B][m]
+ *   x       [B][n], y [B][m], f0 [B][12]
+ *
+ * Conventions: functions return 0 on success, a negative MPCQ_E* code on an
+ * API error (message via mpcq_last_error()).  Per-instance outcomes are
+ * reported through the status array (OSQP codes, see MPCQ_STATUS_*).
+ * Inputs are never mutated.  Calls are blocking unless MPCQ_FLAG_ASYNC.
+ */
+#ifndef MPCQ_H
+#define MPCQ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCQ_ABI_VERSION 1
+
+/* error codes (return values) */
+#define MPCQ_OK 0
+#define MPCQ_E_INVALID (-1)   /* bad argument */
+#define MPCQ_E_DEVICE (-2)    /* HIP runtime error */
+#define MPCQ_E_NOMEM (-3)     /* allocation failed */
+#define MPCQ_E_UNSUPPORTED (-4) /* horizon N not compiled in */
+
+/* per-instance status (OSQP 0.6 status values, plus formulation errors) */
+#define MPCQ_STATUS_SOLVED 1
+#define MPCQ_STATUS_SOLVED_INACCURATE 2
+#define MPCQ_STATUS_MAX_ITER_REACHED (-2)
+#define MPCQ_STATUS_NONFINITE (-10)      /* NaN/Inf reached the solver */
+#define MPCQ_STATUS_BAD_GAIT (-11)       /* fsteps durations: no terminator / sum != N / NaN */
+#define MPCQ_STATUS_FACTOR_FAILED (-12)  /* KKT block lost positive definiteness */
+
+/* flags */
+#define MPCQ_FLAG_DEVICE_PTRS 1u  /* every array argument is a device pointer on ctx's device */
+#define MPCQ_FLAG_ASYNC 2u        /* do not synchronise the stream before returning (device ptrs only) */
+
+/* formulation mode (MPC.py:491-494) */
+#define MPCQ_MODE_UPDATE 0  /* k > 0: update_ML/update_NK with fsteps footholds */
+#define MPCQ_MODE_SETUP 1   /* k == 0: create_ML/create_NK with the default footholds */
+
+/*
+ * Parameters.  mpcq_default_params() fills the reference constants:
+ * dt 0.02, mass 2.50000279 (MPC.py:28), inertia gI (MPC.py:35-37), mu 0.9
+ * (MPC.py:39), fz_max 25 (MPC.py:228), g 9.81 (MPC.py:201), state weights
+ * (MPC.py:255-266), force weight 1e-5 (MPC.py:273-275), default footholds
+ * (MPC.py:67-70) and the OSQP 0.6 settings used by MPC.py:414-416
+ * (eps_abs = eps_rel = 1e-7, every other setting at the library default).
+ */
+typedef struct mpcq_params {
+  /* --- formulation --- */
+  double dt;
+  double mass;
+  double gI[9];             /* row-major 3x3 body inertia */
+  double mu;
+  double fz_max;
+  double gravity;
+  double state_weights[12]; /* P diagonal for [pos, rpy, linvel, angvel] */
+  double force_weight;      /* P diagonal for every force component */
+  double footholds[12];     /* default footholds, row-major 3x4 (setup mode) */
+  /* --- OSQP settings --- */
+  double rho;               /* 0.1 */
+  double sigma;             /* 1e-6 */
+  double alpha;             /* 1.6 */
+  double eps_abs;           /* 1e-7 */
+  double eps_rel;           /* 1e-7 */
+  double adaptive_rho_tolerance; /* 5 */
+  double delta;             /* polish regularisation 1e-6 */
+  int32_t max_iter;         /* 4000 */
+  int32_t check_termination;/* 25 */
+  int32_t adaptive_rho;     /* 1 */
+  int32_t adaptive_rho_interval; /* 100 = OSQP's non-timed rule (4 x check_termination) */
+  int32_t scaling;          /* 10 Ruiz iterations */
+  int32_t polish;           /* 0 off (OSQP default); 1 after SOLVED (OSQP); 2 also after
+                               SOLVED_INACCURATE / MAX_ITER (status upgraded if it then meets eps) */
+  int32_t polish_refine_iter; /* 3 */
+  int32_t polish_rounds;    /* 1 = OSQP's single active-set guess; >1 iterates the
+                               guess (primal-dual active set) until it repeats */
+  int32_t reserved[8];
+} mpcq_params;
+
+typedef struct mpcq_ctx mpcq_ctx;
+
+/* ---- metadata / pattern -------------------------------------------------- */
+int mpcq_abi_version(void);
+void mpcq_default_params(mpcq_params* p);
+/* Dimensions for horizon N: n = 24N, m = 44N, nnz = 126N - 18. */
+int mpcq_dims(int n_steps, int32_t* n, int32_t* m, int32_t* nnz);
+/* CSC pattern of MPC.create_ML (MPC.py:98-151): indptr[n+1], indices[nnz]. */
+int mpcq_pattern(int n_steps, int32_t* indptr, int32_t* indices);
+/* Horizons compiled into the HIP engine (writes up to cap values). */
+int mpcq_supported_horizons(int32_t* out, int cap);
+const char* mpcq_last_error(void);
+
+/* ---- context --------------------------------------------------------------
+ * Replaces MPC.MPC(dt, n_steps, T_gait) (MPC.py:22-82) + osqp.OSQP() (MPC.py:73).
+ * One context per (device, host thread).  The context owns device scratch. */
+int mpcq_create(int device, int n_steps, const mpcq_params* params, mpcq_ctx** out);
+int mpcq_destroy(mpcq_ctx* ctx);
+/* HIP stream (hipStream_t passed as void*) for subsequent launches; NULL = ctx's own stream. */
+int mpcq_set_stream(mpcq_ctx* ctx, void* stream);
+/* Device time of the last launch of each kernel (ms, hipEvent timing on ctx's stream). */
+int mpcq_last_kernel_ms(mpcq_ctx* ctx, double* formulate_ms, double* solve_ms);
+
+/* ---- formulation -----------------------------------------------------------
+ * Replaces MPC.construct_gait + update_matrices (MPC.py:635-652, 290-378) in
+ * MODE_UPDATE, and construct_gait + create_matrices (MPC.py:84-234) in
+ * MODE_SETUP: writes A.data (CSC order), l and u for each instance.
+ * status[b] = 0 or MPCQ_STATUS_BAD_GAIT. */
+int mpcq_formulate_batch(mpcq_ctx* ctx, int64_t batch, const double* xref,
+                         const double* fsteps, int mode, double* Ax, double* l,
+                         double* u, int32_t* status, uint32_t flags);
+
+/* ---- QP solve --------------------------------------------------------------
+ * Replaces osqp.OSQP.update(Ax=, l=, u=) + warm_start(x=) + solve()
+ * (MPC.py:419-428; osqp 0.6 ADMM).  P, q come from params (constant).
+ * warm_x [B][n], warm_y [B][m], rho_in [B] are optional (NULL = cold start,
+ * rho = params.rho).  x, y, rho_out, iters optional outputs (NULL = skip). */
+int mpcq_qp_solve_batch(mpcq_ctx* ctx, int64_t batch, const double* Ax,
+                        const double* l, const double* u, const double* warm_x,
+                        const double* warm_y, const double* rho_in, double* x,
+                        double* y, int32_t* status, int32_t* iters,
+                        double* rho_out, uint32_t flags);
+
+/* ---- fused hot path --------------------------------------------------------
+ * Replaces MPC.run(k, xref, fsteps) (MPC.py:460-514) for a batch: formulation
+ * + OSQP solve + retrieve_result (MPC.py:432-458) in one launch.
+ * f0 [B][12] = f_applied; x [B][n] optional; y [B][m] optional. */
+int mpcq_solve_batch(mpcq_ctx* ctx, int64_t batch, const double* xref,
+                     const double* fsteps, int mode, const double* warm_x,
+                     const double* warm_y, double* f0, double* x, double* y,
+                     int32_t* status, int32_t* iters, uint32_t flags);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCQ_H */

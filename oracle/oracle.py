@@ -1,0 +1,169 @@
+"""ctypes binding of the CPU restatement (oracle/mpcq_oracle.c).
+
+TEST INFRASTRUCTURE ONLY.  Imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, always as the checker; the product package
+(mpc-tsid_amd/) never imports it.
+
+The restatement follows the reference MPC.py formulation (MPC.py:98-378,
+611-652) and the OSQP 0.6 ADMM that MPC.py:413-428 calls; see the C file's
+header for the exact list and DESIGN.md for how it is pinned.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+
+class Params(C.Structure):
+    """Mirror of struct mpcq_params (include/mpcq.h)."""
+
+    _fields_ = [
+        ("dt", C.c_double),
+        ("mass", C.c_double),
+        ("gI", C.c_double * 9),
+        ("mu", C.c_double),
+        ("fz_max", C.c_double),
+        ("gravity", C.c_double),
+        ("state_weights", C.c_double * 12),
+        ("force_weight", C.c_double),
+        ("footholds", C.c_double * 12),
+        ("rho", C.c_double),
+        ("sigma", C.c_double),
+        ("alpha", C.c_double),
+        ("eps_abs", C.c_double),
+        ("eps_rel", C.c_double),
+        ("adaptive_rho_tolerance", C.c_double),
+        ("delta", C.c_double),
+        ("max_iter", C.c_int32),
+        ("check_termination", C.c_int32),
+        ("adaptive_rho", C.c_int32),
+        ("adaptive_rho_interval", C.c_int32),
+        ("scaling", C.c_int32),
+        ("polish", C.c_int32),
+        ("polish_refine_iter", C.c_int32),
+        ("polish_rounds", C.c_int32),
+        ("reserved", C.c_int32 * 8),
+    ]
+
+
+def build(force: bool = False) -> str:
+    """Compile liboracle.so with the Makefile next to this file."""
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(_LIB_PATH)
+        dp = C.POINTER(C.c_double)
+        ip = C.POINTER(C.c_int32)
+        L.oracle_default_params.argtypes = [C.POINTER(Params)]
+        L.oracle_pattern.argtypes = [C.c_int, ip, ip]
+        L.oracle_formulate.argtypes = [C.POINTER(Params), C.c_int, dp, dp, C.c_int, dp, dp, dp]
+        L.oracle_qp_solve.argtypes = [C.POINTER(Params), C.c_int, dp, dp, dp, dp, dp, dp,
+                                      dp, dp, ip, ip, dp, ip]
+        L.oracle_solve_batch.argtypes = [C.POINTER(Params), C.c_int, C.c_int64, dp, dp, C.c_int,
+                                         dp, dp, ip, ip, C.c_int]
+        L.oracle_num_threads.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def default_params(**overrides) -> Params:
+    p = Params()
+    lib().oracle_default_params(C.byref(p))
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    return p
+
+
+def dims(N: int):
+    return 24 * N, 44 * N, 126 * N - 18
+
+
+def _dp(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _ip(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def pattern(N: int):
+    n, m, nnz = dims(N)
+    indptr = np.zeros(n + 1, np.int32)
+    indices = np.zeros(nnz, np.int32)
+    lib().oracle_pattern(N, _ip(indptr), _ip(indices))
+    return indptr, indices
+
+
+def formulate(xref, fsteps, mode: int = 0, params: Params | None = None):
+    """One instance: returns (Ax, l, u) or raises ValueError on a bad gait."""
+    xref = np.ascontiguousarray(xref, np.float64)
+    fsteps = np.ascontiguousarray(fsteps, np.float64)
+    N = xref.shape[1] - 1
+    n, m, nnz = dims(N)
+    Ax = np.zeros(nnz)
+    l = np.zeros(m)
+    u = np.zeros(m)
+    p = params or default_params()
+    st = lib().oracle_formulate(C.byref(p), N, _dp(xref), _dp(fsteps), mode, _dp(Ax), _dp(l), _dp(u))
+    if st != 0:
+        raise ValueError(f"bad gait (status {st})")
+    return Ax, l, u
+
+
+def qp_solve(N, Ax, l, u, params: Params | None = None, warm_x=None, warm_y=None, rho=None):
+    """One QP: returns dict(x, y, status, iters, rho, rho_updates, polish)."""
+    n, m, nnz = dims(N)
+    Ax = np.ascontiguousarray(Ax, np.float64)
+    l = np.ascontiguousarray(l, np.float64)
+    u = np.ascontiguousarray(u, np.float64)
+    x = np.zeros(n)
+    y = np.zeros(m)
+    st = np.zeros(1, np.int32)
+    it = np.zeros(1, np.int32)
+    rho_out = np.zeros(1)
+    info = np.zeros(3, np.int32)
+    rho_in = None if rho is None else np.array([rho], np.float64)
+    wx = None if warm_x is None else np.ascontiguousarray(warm_x, np.float64)
+    wy = None if warm_y is None else np.ascontiguousarray(warm_y, np.float64)
+    p = params or default_params()
+    lib().oracle_qp_solve(C.byref(p), N, _dp(Ax), _dp(l), _dp(u), _dp(wx), _dp(wy), _dp(rho_in),
+                          _dp(x), _dp(y), _ip(st), _ip(it), _dp(rho_out), _ip(info))
+    return dict(x=x, y=y, status=int(st[0]), iters=int(it[0]), rho=float(rho_out[0]),
+                rho_updates=int(info[1]), polish=int(info[2]))
+
+
+def solve_batch(xref, fsteps, mode: int = 0, params: Params | None = None, nthreads: int = 0,
+                want_x: bool = False):
+    """Batched formulation + solve on host threads (OpenMP)."""
+    xref = np.ascontiguousarray(xref, np.float64)
+    fsteps = np.ascontiguousarray(fsteps, np.float64)
+    B = xref.shape[0]
+    N = xref.shape[2] - 1
+    n, m, nnz = dims(N)
+    f0 = np.zeros((B, 12))
+    x = np.zeros((B, n)) if want_x else None
+    st = np.zeros(B, np.int32)
+    it = np.zeros(B, np.int32)
+    p = params or default_params()
+    lib().oracle_solve_batch(C.byref(p), N, B, _dp(xref), _dp(fsteps), mode, _dp(f0), _dp(x),
+                             _ip(st), _ip(it), nthreads)
+    return dict(f0=f0, x=x, status=st, iters=it)
+
+
+def num_threads() -> int:
+    return int(lib().oracle_num_threads())

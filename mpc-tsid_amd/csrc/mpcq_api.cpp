@@ -1,0 +1,392 @@
+// mpcq_api.cpp — host side of the C ABI declared in include/mpcq.h.
+//
+// Owns HIP contexts, device staging buffers for host-pointer calls, stream
+// and event handling.  All numerics run in the HIP kernels
+// (mpcq_kernels.hip); there is no CPU fallback: a missing device is an error.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+
+#include "mpcq_internal.h"
+
+struct mpcq_ctx {
+  int device = 0;
+  int N = 0;
+  mpcq_params p{};
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  void* arena = nullptr;
+  size_t arena_bytes = 0;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool have_form = false, have_solve = false;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(MPCQ_E_DEVICE, "%s failed: %s", #expr, hipGetErrorString(e_));        \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int check_params(const mpcq_params* p) {
+  if (!p) return fail(MPCQ_E_INVALID, "params is NULL");
+  if (!(p->dt > 0) || !(p->mass > 0)) return fail(MPCQ_E_INVALID, "dt and mass must be > 0");
+  if (!(p->rho > 0) || !(p->sigma > 0) || !(p->alpha > 0 && p->alpha < 2))
+    return fail(MPCQ_E_INVALID, "need rho > 0, sigma > 0, 0 < alpha < 2");
+  if (!(p->eps_abs >= 0) || !(p->eps_rel >= 0)) return fail(MPCQ_E_INVALID, "eps must be >= 0");
+  if (p->max_iter < 1 || p->check_termination < 0 || p->scaling < 0 || p->adaptive_rho_interval < 0)
+    return fail(MPCQ_E_INVALID, "max_iter >= 1, check_termination/scaling/interval >= 0");
+  if (!(p->adaptive_rho_tolerance >= 1)) return fail(MPCQ_E_INVALID, "adaptive_rho_tolerance >= 1");
+  if (!(p->force_weight > 0)) return fail(MPCQ_E_INVALID, "force_weight must be > 0");
+  for (int i = 0; i < 12; ++i)
+    if (!(p->state_weights[i] > 0)) return fail(MPCQ_E_INVALID, "state weights must be > 0");
+  return MPCQ_OK;
+}
+
+// Stage the listed host arrays into the context arena.  Each entry: host
+// pointer, byte count, direction (1 = in, 2 = out).  Returns device pointers.
+struct Xfer {
+  const void* host_in;
+  void* host_out;
+  size_t bytes;
+  void* dev;
+};
+
+int ensure_arena(mpcq_ctx* c, size_t bytes) {
+  if (bytes <= c->arena_bytes) return MPCQ_OK;
+  if (c->arena) HIP_TRY(hipFree(c->arena));
+  c->arena = nullptr;
+  c->arena_bytes = 0;
+  size_t want = bytes + bytes / 4;
+  if (hipMalloc(&c->arena, want) != hipSuccess) {
+    c->arena = nullptr;
+    return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) failed", want);
+  }
+  c->arena_bytes = want;
+  return MPCQ_OK;
+}
+
+int stage(mpcq_ctx* c, Xfer* xs, int nx) {
+  size_t tot = 0;
+  for (int i = 0; i < nx; ++i)
+    if (xs[i].host_in || xs[i].host_out) tot += (xs[i].bytes + 255) & ~size_t(255);
+  int rc = ensure_arena(c, tot);
+  if (rc) return rc;
+  size_t off = 0;
+  for (int i = 0; i < nx; ++i) {
+    xs[i].dev = nullptr;
+    if (!(xs[i].host_in || xs[i].host_out)) continue;
+    xs[i].dev = (char*)c->arena + off;
+    off += (xs[i].bytes + 255) & ~size_t(255);
+    if (xs[i].host_in)
+      HIP_TRY(hipMemcpyAsync(xs[i].dev, xs[i].host_in, xs[i].bytes, hipMemcpyHostToDevice, c->stream));
+  }
+  return MPCQ_OK;
+}
+
+int unstage(mpcq_ctx* c, Xfer* xs, int nx) {
+  for (int i = 0; i < nx; ++i)
+    if (xs[i].host_out)
+      HIP_TRY(hipMemcpyAsync(xs[i].host_out, xs[i].dev, xs[i].bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPCQ_OK;
+}
+
+int check_ctx(mpcq_ctx* c, int64_t batch) {
+  if (!c) return fail(MPCQ_E_INVALID, "ctx is NULL");
+  if (batch < 0 || batch > (int64_t)0x7fffffff) return fail(MPCQ_E_INVALID, "bad batch %lld", (long long)batch);
+  return MPCQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpcq_abi_version(void) { return MPCQ_ABI_VERSION; }
+
+// Reference constants: MPC.py:25-39 (dt from main.py:20, mass, gI, mu), 67-70
+// (footholds), 201 (g), 228 (fz_max), 255-275 (weights); OSQP settings
+// MPC.py:414-416 + osqp 0.6 defaults.
+void mpcq_default_params(mpcq_params* p) {
+  if (!p) return;
+  memset(p, 0, sizeof(*p));
+  p->dt = 0.02;
+  p->mass = 2.50000279;
+  const double gI[9] = {3.09249e-2, -8.00101e-7, 1.865287e-5, -8.00101e-7, 5.106100e-2,
+                        1.245813e-4, 1.865287e-5, 1.245813e-4, 6.939757e-2};
+  memcpy(p->gI, gI, sizeof(gI));
+  p->mu = 0.9;
+  p->fz_max = 25.0;
+  p->gravity = 9.81;
+  const double w[12] = {0.1, 0.1, 1.0, 0.11, 0.11, 0.11, 2.0 * sqrt(0.1), 2.0 * sqrt(0.1),
+                        2.0 * sqrt(1.0), 0.05 * sqrt(0.11), 0.05 * sqrt(0.11), 0.05 * sqrt(0.11)};
+  memcpy(p->state_weights, w, sizeof(w));
+  p->force_weight = 1.0e-5;
+  const double fh[12] = {0.19, 0.19, -0.19, -0.19, 0.15005, -0.15005,
+                         0.15005, -0.15005, 0.0, 0.0, 0.0, 0.0};
+  memcpy(p->footholds, fh, sizeof(fh));
+  p->rho = 0.1;
+  p->sigma = 1e-6;
+  p->alpha = 1.6;
+  p->eps_abs = 1e-7;
+  p->eps_rel = 1e-7;
+  p->adaptive_rho_tolerance = 5.0;
+  p->delta = 1e-6;
+  p->max_iter = 4000;
+  p->check_termination = 25;
+  p->adaptive_rho = 1;
+  p->adaptive_rho_interval = 100;
+  p->scaling = 10;
+  p->polish = 0;
+  p->polish_refine_iter = 3;
+  p->polish_rounds = 1;
+}
+
+int mpcq_dims(int N, int32_t* n, int32_t* m, int32_t* nnz) {
+  if (N < 2) return fail(MPCQ_E_INVALID, "n_steps must be >= 2");
+  if (n) *n = 24 * N;
+  if (m) *m = 44 * N;
+  if (nnz) *nnz = 126 * N - 18;
+  return MPCQ_OK;
+}
+
+// CSC pattern of the dense matrix built by MPC.create_ML (MPC.py:103-151):
+// state columns (-I of dynamics row k, A of dynamics row k+1), then per stage,
+// foot and component the force column (dt/m row, B rows 9-11, swing row,
+// friction rows).
+int mpcq_pattern(int N, int32_t* indptr, int32_t* indices) {
+  if (N < 2 || !indptr || !indices) return fail(MPCQ_E_INVALID, "bad arguments");
+  int pos = 0;
+  for (int c = 0; c < 12 * N; ++c) {
+    const int k = c / 12, i = c % 12;
+    indptr[c] = pos;
+    indices[pos++] = c;
+    if (k < N - 1) {
+      if (i >= 6) indices[pos++] = 12 * (k + 1) + i - 6;
+      indices[pos++] = 12 * (k + 1) + i;
+    }
+  }
+  for (int k = 0; k < N; ++k)
+    for (int f = 0; f < 4; ++f)
+      for (int c = 0; c < 3; ++c) {
+        indptr[12 * N + 12 * k + 3 * f + c] = pos;
+        indices[pos++] = 12 * k + 6 + c;
+        for (int r = 9; r < 12; ++r) indices[pos++] = 12 * k + r;
+        indices[pos++] = 12 * N + 12 * k + 3 * f + c;
+        const int fr = 24 * N + 20 * k + 5 * f;
+        if (c == 0) { indices[pos++] = fr; indices[pos++] = fr + 1; }
+        else if (c == 1) { indices[pos++] = fr + 2; indices[pos++] = fr + 3; }
+        else for (int t = 0; t < 5; ++t) indices[pos++] = fr + t;
+      }
+  indptr[24 * N] = pos;
+  return MPCQ_OK;
+}
+
+int mpcq_supported_horizons(int32_t* out, int cap) { return mpcq::supported_horizons(out, cap); }
+
+const char* mpcq_last_error(void) { return g_err.c_str(); }
+
+int mpcq_create(int device, int n_steps, const mpcq_params* params, mpcq_ctx** out) {
+  if (!out) return fail(MPCQ_E_INVALID, "out is NULL");
+  *out = nullptr;
+  if (!mpcq::horizon_supported(n_steps))
+    return fail(MPCQ_E_UNSUPPORTED, "horizon N=%d not compiled in (supported: 16, 32)", n_steps);
+  mpcq_params p;
+  if (params) p = *params;
+  else mpcq_default_params(&p);
+  int rc = check_params(&p);
+  if (rc) return rc;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(MPCQ_E_DEVICE, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(MPCQ_E_INVALID, "device %d out of range (%d)", device, ndev);
+  DeviceGuard g(device);
+  mpcq_ctx* c = new mpcq_ctx();
+  c->device = device;
+  c->N = n_steps;
+  c->p = p;
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return fail(MPCQ_E_DEVICE, "hipStreamCreate failed");
+  }
+  c->stream = c->own_stream;
+  for (auto& e : c->ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      mpcq_destroy(c);
+      return fail(MPCQ_E_DEVICE, "hipEventCreate failed");
+    }
+  *out = c;
+  return MPCQ_OK;
+}
+
+int mpcq_destroy(mpcq_ctx* c) {
+  if (!c) return MPCQ_OK;
+  DeviceGuard g(c->device);
+  if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+  if (c->arena) (void)hipFree(c->arena);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return MPCQ_OK;
+}
+
+int mpcq_set_stream(mpcq_ctx* c, void* stream) {
+  if (!c) return fail(MPCQ_E_INVALID, "ctx is NULL");
+  c->stream = stream ? (hipStream_t)stream : c->own_stream;
+  return MPCQ_OK;
+}
+
+int mpcq_last_kernel_ms(mpcq_ctx* c, double* fms, double* sms) {
+  if (!c) return fail(MPCQ_E_INVALID, "ctx is NULL");
+  DeviceGuard g(c->device);
+  float ms = 0.f;
+  if (fms) {
+    *fms = -1.0;
+    if (c->have_form) {
+      HIP_TRY(hipEventSynchronize(c->ev[1]));
+      HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+      *fms = ms;
+    }
+  }
+  if (sms) {
+    *sms = -1.0;
+    if (c->have_solve) {
+      HIP_TRY(hipEventSynchronize(c->ev[3]));
+      HIP_TRY(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+      *sms = ms;
+    }
+  }
+  return MPCQ_OK;
+}
+
+int mpcq_formulate_batch(mpcq_ctx* c, int64_t B, const double* xref, const double* fsteps, int mode,
+                         double* Ax, double* l, double* u, int32_t* status, uint32_t flags) {
+  int rc = check_ctx(c, B);
+  if (rc) return rc;
+  if (!xref || !fsteps || !Ax || !l || !u) return fail(MPCQ_E_INVALID, "NULL array");
+  if (mode != MPCQ_MODE_UPDATE && mode != MPCQ_MODE_SETUP) return fail(MPCQ_E_INVALID, "bad mode");
+  if (B == 0) return MPCQ_OK;
+  DeviceGuard g(c->device);
+  const int N = c->N;
+  const size_t n12 = 12 * (N + 1), nnz = 126 * N - 18, m = 44 * N;
+  mpcq::LaunchArgs a{};
+  a.batch = B;
+  a.mode = mode;
+  const bool dev = flags & MPCQ_FLAG_DEVICE_PTRS;
+  Xfer xs[6] = {{xref, nullptr, B * n12 * 8, nullptr}, {fsteps, nullptr, (size_t)B * 260 * 8, nullptr},
+                {nullptr, Ax, B * nnz * 8, nullptr},   {nullptr, l, B * m * 8, nullptr},
+                {nullptr, u, B * m * 8, nullptr},      {nullptr, status, (size_t)B * 4, nullptr}};
+  if (!dev) {
+    rc = stage(c, xs, 6);
+    if (rc) return rc;
+    a.xref = (const double*)xs[0].dev; a.fsteps = (const double*)xs[1].dev;
+    a.Ax_out = (double*)xs[2].dev; a.l_out = (double*)xs[3].dev; a.u_out = (double*)xs[4].dev;
+    a.status = (int32_t*)xs[5].dev;
+  } else {
+    a.xref = xref; a.fsteps = fsteps; a.Ax_out = Ax; a.l_out = l; a.u_out = u; a.status = status;
+  }
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  HIP_TRY(mpcq::launch_formulate(N, c->p, a, c->stream));
+  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+  c->have_form = true;
+  if (!dev) return unstage(c, xs, 6);
+  if (!(flags & MPCQ_FLAG_ASYNC)) HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPCQ_OK;
+}
+
+static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, const double* fsteps,
+                        int mode, const double* Ax, const double* l, const double* u,
+                        const double* warm_x, const double* warm_y, const double* rho_in, double* f0,
+                        double* x, double* y, int32_t* status, int32_t* iters, double* rho_out,
+                        uint32_t flags) {
+  int rc = check_ctx(c, B);
+  if (rc) return rc;
+  if (B == 0) return MPCQ_OK;
+  DeviceGuard g(c->device);
+  const int N = c->N;
+  const size_t n = 24 * N, m = 44 * N, nnz = 126 * N - 18, n12 = 12 * (N + 1);
+  mpcq::LaunchArgs a{};
+  a.batch = B;
+  a.mode = mode;
+  const bool dev = flags & MPCQ_FLAG_DEVICE_PTRS;
+  enum { XR, FS, AX, L, U, WX, WY, RI, F0, X, Y, ST, IT, RO, NX };
+  Xfer xs[NX] = {
+      {xref, nullptr, B * n12 * 8, nullptr},      {fsteps, nullptr, (size_t)B * 260 * 8, nullptr},
+      {Ax, nullptr, B * nnz * 8, nullptr},        {l, nullptr, B * m * 8, nullptr},
+      {u, nullptr, B * m * 8, nullptr},           {warm_x, nullptr, B * n * 8, nullptr},
+      {warm_y, nullptr, B * m * 8, nullptr},      {rho_in, nullptr, (size_t)B * 8, nullptr},
+      {nullptr, f0, (size_t)B * 12 * 8, nullptr}, {nullptr, x, B * n * 8, nullptr},
+      {nullptr, y, B * m * 8, nullptr},           {nullptr, status, (size_t)B * 4, nullptr},
+      {nullptr, iters, (size_t)B * 4, nullptr},   {nullptr, rho_out, (size_t)B * 8, nullptr}};
+  if (!dev) {
+    rc = stage(c, xs, NX);
+    if (rc) return rc;
+    a.xref = (const double*)xs[XR].dev; a.fsteps = (const double*)xs[FS].dev;
+    a.Ax = (const double*)xs[AX].dev; a.l = (const double*)xs[L].dev; a.u = (const double*)xs[U].dev;
+    a.warm_x = (const double*)xs[WX].dev; a.warm_y = (const double*)xs[WY].dev;
+    a.rho_in = (const double*)xs[RI].dev;
+    a.f0 = (double*)xs[F0].dev; a.x = (double*)xs[X].dev; a.y = (double*)xs[Y].dev;
+    a.status = (int32_t*)xs[ST].dev; a.iters = (int32_t*)xs[IT].dev; a.rho_out = (double*)xs[RO].dev;
+  } else {
+    a.xref = xref; a.fsteps = fsteps; a.Ax = Ax; a.l = l; a.u = u;
+    a.warm_x = warm_x; a.warm_y = warm_y; a.rho_in = rho_in;
+    a.f0 = f0; a.x = x; a.y = y; a.status = status; a.iters = iters; a.rho_out = rho_out;
+  }
+  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  HIP_TRY(mpcq::launch_solve(N, fused, c->p, a, c->stream));
+  HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+  c->have_solve = true;
+  if (!dev) return unstage(c, xs, NX);
+  if (!(flags & MPCQ_FLAG_ASYNC)) HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPCQ_OK;
+}
+
+int mpcq_qp_solve_batch(mpcq_ctx* c, int64_t B, const double* Ax, const double* l, const double* u,
+                        const double* warm_x, const double* warm_y, const double* rho_in, double* x,
+                        double* y, int32_t* status, int32_t* iters, double* rho_out, uint32_t flags) {
+  if (!Ax || !l || !u) return fail(MPCQ_E_INVALID, "Ax, l, u are required");
+  return solve_common(c, B, false, nullptr, nullptr, 0, Ax, l, u, warm_x, warm_y, rho_in, nullptr, x,
+                      y, status, iters, rho_out, flags);
+}
+
+int mpcq_solve_batch(mpcq_ctx* c, int64_t B, const double* xref, const double* fsteps, int mode,
+                     const double* warm_x, const double* warm_y, double* f0, double* x, double* y,
+                     int32_t* status, int32_t* iters, uint32_t flags) {
+  if (!xref || !fsteps) return fail(MPCQ_E_INVALID, "xref, fsteps are required");
+  if (mode != MPCQ_MODE_UPDATE && mode != MPCQ_MODE_SETUP) return fail(MPCQ_E_INVALID, "bad mode");
+  return solve_common(c, B, true, xref, fsteps, mode, nullptr, nullptr, nullptr, warm_x, warm_y,
+                      nullptr, f0, x, y, status, iters, nullptr, flags);
+}
+
+}  // extern "C"

@@ -1,0 +1,145 @@
+"""ctypes binding of libmpcq.so (the C ABI in include/mpcq.h).
+
+The shared library is built in-tree (mpc-tsid_amd/csrc/Makefile ->
+mpc-tsid_amd/mpcq/libmpcq.so) and loaded from here.  There is no fallback:
+if the library or a HIP device is missing, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmpcq.so")
+CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+
+# return codes / status / flags / modes (include/mpcq.h)
+OK = 0
+E_INVALID, E_DEVICE, E_NOMEM, E_UNSUPPORTED = -1, -2, -3, -4
+STATUS_SOLVED = 1
+STATUS_SOLVED_INACCURATE = 2
+STATUS_MAX_ITER_REACHED = -2
+STATUS_NONFINITE = -10
+STATUS_BAD_GAIT = -11
+STATUS_FACTOR_FAILED = -12
+FLAG_DEVICE_PTRS = 1
+FLAG_ASYNC = 2
+MODE_UPDATE = 0
+MODE_SETUP = 1
+
+EXPORTS = ("mpcq_abi_version", "mpcq_default_params", "mpcq_dims", "mpcq_pattern",
+           "mpcq_supported_horizons", "mpcq_last_error", "mpcq_create", "mpcq_destroy",
+           "mpcq_set_stream", "mpcq_last_kernel_ms", "mpcq_formulate_batch",
+           "mpcq_qp_solve_batch", "mpcq_solve_batch")
+
+
+class MpcqError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mpcq error {code}: {msg}")
+        self.code = code
+
+
+class Params(C.Structure):
+    """struct mpcq_params (include/mpcq.h)."""
+
+    _fields_ = [
+        ("dt", C.c_double),
+        ("mass", C.c_double),
+        ("gI", C.c_double * 9),
+        ("mu", C.c_double),
+        ("fz_max", C.c_double),
+        ("gravity", C.c_double),
+        ("state_weights", C.c_double * 12),
+        ("force_weight", C.c_double),
+        ("footholds", C.c_double * 12),
+        ("rho", C.c_double),
+        ("sigma", C.c_double),
+        ("alpha", C.c_double),
+        ("eps_abs", C.c_double),
+        ("eps_rel", C.c_double),
+        ("adaptive_rho_tolerance", C.c_double),
+        ("delta", C.c_double),
+        ("max_iter", C.c_int32),
+        ("check_termination", C.c_int32),
+        ("adaptive_rho", C.c_int32),
+        ("adaptive_rho_interval", C.c_int32),
+        ("scaling", C.c_int32),
+        ("polish", C.c_int32),
+        ("polish_refine_iter", C.c_int32),
+        ("polish_rounds", C.c_int32),
+        ("reserved", C.c_int32 * 8),
+    ]
+
+    def as_dict(self):
+        out = {}
+        for name, _ in self._fields_:
+            v = getattr(self, name)
+            out[name] = list(v) if hasattr(v, "__len__") else v
+        return out
+
+
+def build(force: bool = False) -> str:
+    """Compile libmpcq.so for gfx950 with hipcc (csrc/Makefile)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", CSRC], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MpcqError(E_DEVICE, f"{LIB_PATH} is missing: run `make -C {CSRC}` (or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    dp, ip, vp = C.POINTER(C.c_double), C.POINTER(C.c_int32), C.c_void_p
+    PP = C.POINTER(Params)
+    L.mpcq_abi_version.restype = C.c_int
+    L.mpcq_default_params.argtypes = [PP]
+    L.mpcq_default_params.restype = None
+    L.mpcq_dims.argtypes = [C.c_int, ip, ip, ip]
+    L.mpcq_pattern.argtypes = [C.c_int, ip, ip]
+    L.mpcq_supported_horizons.argtypes = [ip, C.c_int]
+    L.mpcq_last_error.restype = C.c_char_p
+    L.mpcq_create.argtypes = [C.c_int, C.c_int, PP, C.POINTER(vp)]
+    L.mpcq_destroy.argtypes = [vp]
+    L.mpcq_set_stream.argtypes = [vp, vp]
+    L.mpcq_last_kernel_ms.argtypes = [vp, dp, dp]
+    L.mpcq_formulate_batch.argtypes = [vp, C.c_int64, vp, vp, C.c_int, vp, vp, vp, vp, C.c_uint32]
+    L.mpcq_qp_solve_batch.argtypes = [vp, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                      C.c_uint32]
+    L.mpcq_solve_batch.argtypes = [vp, C.c_int64, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp,
+                                   C.c_uint32]
+    for name in ("mpcq_dims", "mpcq_pattern", "mpcq_supported_horizons", "mpcq_create",
+                 "mpcq_destroy", "mpcq_set_stream", "mpcq_last_kernel_ms", "mpcq_formulate_batch",
+                 "mpcq_qp_solve_batch", "mpcq_solve_batch"):
+        getattr(L, name).restype = C.c_int
+    _lib = L
+    return L
+
+
+def check(rc: int):
+    if rc != OK:
+        msg = lib().mpcq_last_error()
+        raise MpcqError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def default_params(**overrides) -> Params:
+    p = Params()
+    lib().mpcq_default_params(C.byref(p))
+    for k, v in overrides.items():
+        if not hasattr(p, k):
+            raise AttributeError(f"unknown parameter {k}")
+        setattr(p, k, v)
+    return p
+
+
+def supported_horizons():
+    buf = (C.c_int32 * 8)()
+    n = lib().mpcq_supported_horizons(buf, 8)
+    return [buf[i] for i in range(min(n, 8))]

@@ -1,0 +1,107 @@
+"""GPU parity: the HIP engine (libmpcq.so through its C ABI) against the oracle
+and the reference-generated golden fixtures.  Run with -m gpu on an MI355X."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FORM_TOL = 1e-13  # formulation (relative, ulp-level: FMA contraction on the GPU)
+
+
+@pytest.fixture(scope="module")
+def mpcq():
+    import mpcq as M
+    return M
+
+
+@pytest.fixture(scope="module")
+def eng16(mpcq):
+    e = mpcq.Engine(16)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def eng32(mpcq):
+    e = mpcq.Engine(32)
+    yield e
+    e.close()
+
+
+def _rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    assert np.array_equal(np.isinf(a), np.isinf(b))
+    fa, fb = np.where(np.isinf(a), 0, a), np.where(np.isinf(b), 0, b)
+    return float((np.abs(fa - fb) / np.maximum(1.0, np.abs(fb))).max(initial=0))
+
+
+@pytest.mark.parametrize("N", [16, 32])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_formulation_vs_reference(N, mode, eng16, eng32, golden16, golden32):
+    e, g = (eng16, golden16) if N == 16 else (eng32, golden32)
+    sfx = "" if mode == 0 else "_setup"
+    r = e.formulate(g["xref"], g["fsteps"], mode)
+    assert (r["status"] == 0).all()
+    err = max(_rel(r["Ax"], g["Ax" + sfx]), _rel(r["l"], g["l" + sfx]), _rel(r["u"], g["u" + sfx]))
+    print(f"N={N} mode={mode} formulation max rel err vs reference {err:.2e}")
+    assert err <= FORM_TOL
+
+
+def test_formulation_vs_oracle_synthetic(eng16, oracle, mpcq):
+    b = mpcq.synth.make_batch(256, 16, gaits=mpcq.synth.GAITS, seed=11)
+    r = eng16.formulate(b["xref"], b["fsteps"], 0)
+    worst = 0.0
+    for i in range(0, 256, 7):
+        Ax, l, u = oracle.formulate(b["xref"][i], b["fsteps"][i], 0)
+        worst = max(worst, _rel(r["Ax"][i], Ax), _rel(r["l"][i], l), _rel(r["u"][i], u))
+    assert worst <= FORM_TOL, worst
+
+
+def test_bad_gait_status(eng16, golden16, mpcq):
+    r = eng16.formulate(np.repeat(golden16["bad_xref"][None], 3, 0), golden16["bad_fsteps"], 0)
+    assert (r["status"] == mpcq.STATUS_BAD_GAIT).all()
+    s = eng16.solve(np.repeat(golden16["bad_xref"][None], 3, 0), golden16["bad_fsteps"], 0)
+    assert (s["status"] == mpcq.STATUS_BAD_GAIT).all()
+    assert np.isnan(s["f0"]).all()
+
+
+@pytest.mark.parametrize("N", [16, 32])
+def test_qp_solve_vs_oracle(N, eng16, eng32, golden16, golden32, oracle):
+    """Same OSQP-0.6 algorithm on the same QP data: statuses and iteration
+    counts agree and the returned forces agree far inside 1e-4."""
+    e, g = (eng16, golden16) if N == 16 else (eng32, golden32)
+    r = e.qp_solve(g["Ax"], g["l"], g["u"])
+    B = g["Ax"].shape[0]
+    same_it = 0
+    errs = []
+    for b in range(B):
+        o = oracle.qp_solve(N, g["Ax"][b], g["l"][b], g["u"][b])
+        same_it += int(o["iters"] == r["iters"][b])
+        errs.append(np.abs(r["x"][b] - o["x"]).max())
+        assert r["status"][b] == o["status"], (b, r["status"][b], o["status"])
+    errs = np.array(errs)
+    print(f"N={N}: iteration counts equal on {same_it}/{B}; max|x-x_oracle| {errs.max():.2e} "
+          f"median {np.median(errs):.2e}; iters {np.median(r['iters'])}")
+    assert same_it >= 0.9 * B
+    assert np.median(errs) < 1e-6
+    assert errs.max() < 1e-4
+
+
+def test_fused_vs_oracle(eng16, oracle, mpcq):
+    b = mpcq.synth.make_batch(64, 16, gaits=mpcq.synth.GAITS, seed=5)
+    r = eng16.solve(b["xref"], b["fsteps"], 0)
+    o = oracle.solve_batch(b["xref"], b["fsteps"], 0, nthreads=8)
+    assert np.array_equal(r["status"], o["status"])
+    err = np.abs(r["f0"] - o["f0"]).max(axis=1)
+    print(f"fused: max|f0-f0_oracle| {err.max():.2e} median {np.median(err):.2e}")
+    assert np.median(err) < 1e-6
+    assert err.max() < 1e-4
+
+
+def test_nonfinite_input(eng16, golden16, mpcq):
+    Ax = golden16["Ax"][:2].copy()
+    Ax[1, 100] = np.nan
+    r = eng16.qp_solve(Ax, golden16["l"][:2], golden16["u"][:2])
+    assert r["status"][0] == mpcq.STATUS_SOLVED
+    assert r["status"][1] == mpcq.STATUS_NONFINITE
+    assert np.isnan(r["x"][1]).all()

@@ -134,12 +134,14 @@ int mpcq_formulate_batch(mpcq_ctx* ctx, int64_t batch, const double* xref,
  * Replaces osqp.OSQP.update(Ax=, l=, u=) + warm_start(x=) + solve()
  * (MPC.py:419-428; osqp 0.6 ADMM).  P, q come from params (constant).
  * warm_x [B][n], warm_y [B][m], rho_in [B] are optional (NULL = cold start,
- * rho = params.rho).  x, y, rho_out, iters optional outputs (NULL = skip). */
+ * rho = params.rho).  x, y, rho_out, iters optional outputs (NULL = skip).
+ * info [B][4] (optional): rho updates (refactorisations after the first),
+ * polish result (0 not run, 1 accepted, -1 rejected), polish rounds run, 0. */
 int mpcq_qp_solve_batch(mpcq_ctx* ctx, int64_t batch, const double* Ax,
                         const double* l, const double* u, const double* warm_x,
                         const double* warm_y, const double* rho_in, double* x,
                         double* y, int32_t* status, int32_t* iters,
-                        double* rho_out, uint32_t flags);
+                        double* rho_out, int32_t* info, uint32_t flags);
 
 /* ---- fused hot path --------------------------------------------------------
  * Replaces MPC.run(k, xref, fsteps) (MPC.py:460-514) for a batch: formulation
@@ -148,7 +150,13 @@ int mpcq_qp_solve_batch(mpcq_ctx* ctx, int64_t batch, const double* Ax,
 int mpcq_solve_batch(mpcq_ctx* ctx, int64_t batch, const double* xref,
                      const double* fsteps, int mode, const double* warm_x,
                      const double* warm_y, double* f0, double* x, double* y,
-                     int32_t* status, int32_t* iters, uint32_t flags);
+                     int32_t* status, int32_t* iters, int32_t* info, uint32_t flags);
+
+/* ---- diagnostics -----------------------------------------------------------
+ * Device buffer [B][16] (uint64) that a diagnostic build of the library
+ * (compiled with -DMPCQ_STAMPS, libmpcq_stamps.so) fills with per-phase
+ * s_memtime cycle counts of thread 0; ignored by the shipped build. */
+int mpcq_debug_set_stamps(mpcq_ctx* ctx, void* device_buffer);
 
 #ifdef __cplusplus
 }

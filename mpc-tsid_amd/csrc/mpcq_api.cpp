@@ -23,6 +23,7 @@ struct mpcq_ctx {
   size_t arena_bytes = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool have_form = false, have_solve = false;
+  uint64_t* stamps = nullptr;
 };
 
 namespace {
@@ -329,7 +330,7 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
                         int mode, const double* Ax, const double* l, const double* u,
                         const double* warm_x, const double* warm_y, const double* rho_in, double* f0,
                         double* x, double* y, int32_t* status, int32_t* iters, double* rho_out,
-                        uint32_t flags) {
+                        int32_t* info, uint32_t flags) {
   int rc = check_ctx(c, B);
   if (rc) return rc;
   if (B == 0) return MPCQ_OK;
@@ -340,7 +341,7 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
   a.batch = B;
   a.mode = mode;
   const bool dev = flags & MPCQ_FLAG_DEVICE_PTRS;
-  enum { XR, FS, AX, L, U, WX, WY, RI, F0, X, Y, ST, IT, RO, NX };
+  enum { XR, FS, AX, L, U, WX, WY, RI, F0, X, Y, ST, IT, RO, IN, NX };
   Xfer xs[NX] = {
       {xref, nullptr, B * n12 * 8, nullptr},      {fsteps, nullptr, (size_t)B * 260 * 8, nullptr},
       {Ax, nullptr, B * nnz * 8, nullptr},        {l, nullptr, B * m * 8, nullptr},
@@ -348,7 +349,8 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
       {warm_y, nullptr, B * m * 8, nullptr},      {rho_in, nullptr, (size_t)B * 8, nullptr},
       {nullptr, f0, (size_t)B * 12 * 8, nullptr}, {nullptr, x, B * n * 8, nullptr},
       {nullptr, y, B * m * 8, nullptr},           {nullptr, status, (size_t)B * 4, nullptr},
-      {nullptr, iters, (size_t)B * 4, nullptr},   {nullptr, rho_out, (size_t)B * 8, nullptr}};
+      {nullptr, iters, (size_t)B * 4, nullptr},   {nullptr, rho_out, (size_t)B * 8, nullptr},
+      {nullptr, info, (size_t)B * 16, nullptr}};
   if (!dev) {
     rc = stage(c, xs, NX);
     if (rc) return rc;
@@ -358,11 +360,14 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
     a.rho_in = (const double*)xs[RI].dev;
     a.f0 = (double*)xs[F0].dev; a.x = (double*)xs[X].dev; a.y = (double*)xs[Y].dev;
     a.status = (int32_t*)xs[ST].dev; a.iters = (int32_t*)xs[IT].dev; a.rho_out = (double*)xs[RO].dev;
+    a.info = (int32_t*)xs[IN].dev;
   } else {
     a.xref = xref; a.fsteps = fsteps; a.Ax = Ax; a.l = l; a.u = u;
     a.warm_x = warm_x; a.warm_y = warm_y; a.rho_in = rho_in;
     a.f0 = f0; a.x = x; a.y = y; a.status = status; a.iters = iters; a.rho_out = rho_out;
+    a.info = info;
   }
+  a.stamps = c->stamps;
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   HIP_TRY(mpcq::launch_solve(N, fused, c->p, a, c->stream));
   HIP_TRY(hipEventRecord(c->ev[3], c->stream));
@@ -374,19 +379,26 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
 
 int mpcq_qp_solve_batch(mpcq_ctx* c, int64_t B, const double* Ax, const double* l, const double* u,
                         const double* warm_x, const double* warm_y, const double* rho_in, double* x,
-                        double* y, int32_t* status, int32_t* iters, double* rho_out, uint32_t flags) {
+                        double* y, int32_t* status, int32_t* iters, double* rho_out, int32_t* info,
+                        uint32_t flags) {
   if (!Ax || !l || !u) return fail(MPCQ_E_INVALID, "Ax, l, u are required");
   return solve_common(c, B, false, nullptr, nullptr, 0, Ax, l, u, warm_x, warm_y, rho_in, nullptr, x,
-                      y, status, iters, rho_out, flags);
+                      y, status, iters, rho_out, info, flags);
 }
 
 int mpcq_solve_batch(mpcq_ctx* c, int64_t B, const double* xref, const double* fsteps, int mode,
                      const double* warm_x, const double* warm_y, double* f0, double* x, double* y,
-                     int32_t* status, int32_t* iters, uint32_t flags) {
+                     int32_t* status, int32_t* iters, int32_t* info, uint32_t flags) {
   if (!xref || !fsteps) return fail(MPCQ_E_INVALID, "xref, fsteps are required");
   if (mode != MPCQ_MODE_UPDATE && mode != MPCQ_MODE_SETUP) return fail(MPCQ_E_INVALID, "bad mode");
   return solve_common(c, B, true, xref, fsteps, mode, nullptr, nullptr, nullptr, warm_x, warm_y,
-                      nullptr, f0, x, y, status, iters, nullptr, flags);
+                      nullptr, f0, x, y, status, iters, nullptr, info, flags);
+}
+
+int mpcq_debug_set_stamps(mpcq_ctx* c, void* buf) {
+  if (!c) return fail(MPCQ_E_INVALID, "ctx is NULL");
+  c->stamps = (uint64_t*)buf;
+  return MPCQ_OK;
 }
 
 }  // extern "C"

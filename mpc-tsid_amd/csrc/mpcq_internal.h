@@ -30,6 +30,7 @@ struct LaunchArgs {
   int32_t* iters;      // [B]
   double* rho_out;     // [B]
   int32_t* info;       // [B][4]: rho updates, polish status, polish rounds, reserved
+  uint64_t* stamps;    // [B][16] diagnostic build only (MPCQ_STAMPS): cycles per phase
 };
 
 // Launchers (mpcq_kernels.hip).  Return hipError_t.

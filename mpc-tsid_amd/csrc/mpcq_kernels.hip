@@ -37,6 +37,16 @@ constexpr double kMinScaling = 1e-4, kMaxScaling = 1e4;
 constexpr double kRhoMin = 1e-6, kRhoMax = 1e6, kRhoEq = 1e3, kRhoTol = 1e-4;
 constexpr double kDivTol = 1e-30;
 
+// Diagnostic build (-DMPCQ_STAMPS): thread 0 accumulates s_memtime deltas per
+// phase into LaunchArgs::stamps.  The shipped build compiles these away.
+#ifdef MPCQ_STAMPS
+#define STAMP_DECL uint64_t st_acc[16] = {}; uint64_t st_last = __builtin_amdgcn_s_memtime();
+#define STAMP(i) do { if (threadIdx.x == 0) { const uint64_t nw_ = __builtin_amdgcn_s_memtime(); st_acc[i] += nw_ - st_last; st_last = nw_; } } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(i) do {} while (0)
+#endif
+
 template <int N>
 struct Geo {
   static constexpr int n = 24 * N, m = 44 * N, nnz = 126 * N - 18;
@@ -466,8 +476,15 @@ __device__ __forceinline__ bool factor(Smem<N>& sh, double (&Si)[4][12]) {
 // ----------------------------------------------------------------------------
 // KKT solve: b in sh.vn (stage ordered) -> w in sh.vn.
 
+#ifdef MPCQ_STAMPS
+#define KKT_STAMP_ARGS , uint64_t (&st_acc)[16], uint64_t& st_last
+#define KKT_STAMP_PASS , st_acc, st_last
+#else
+#define KKT_STAMP_ARGS
+#define KKT_STAMP_PASS
+#endif
 template <int N>
-__device__ __forceinline__ void kkt_solve(Smem<N>& sh, const double (&Si)[4][12]) {
+__device__ __forceinline__ void kkt_solve(Smem<N>& sh, const double (&Si)[4][12] KKT_STAMP_ARGS) {
   constexpr int NW = Geo<N>::NW;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = lane >> 1, h = lane & 1;
@@ -485,6 +502,7 @@ __device__ __forceinline__ void kkt_solve(Smem<N>& sh, const double (&Si)[4][12]
     if (lane >= 24 && lane < 48 && h == 0) sh.sv[12 * k + r - 12] = acc;
   }
   __syncthreads();
+  STAMP(4);
   // forward recurrence s_k = alpha_k - Gamma_k s_{k-1} (wave 0)
   if (wv == 0) {
     const int i = lane >> 2, q = lane & 3;
@@ -507,6 +525,7 @@ __device__ __forceinline__ void kkt_solve(Smem<N>& sh, const double (&Si)[4][12]
     }
   }
   __syncthreads();
+  STAMP(5);
   // phase B: t_k = S_k^{-1}(b_k - C_k s_{k-1}); beta_k = C_k' t_k
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -569,6 +588,7 @@ __device__ __forceinline__ void kkt_solve(Smem<N>& sh, const double (&Si)[4][12]
     wave_sync();
   }
   __syncthreads();
+  STAMP(6);
   // backward recurrence v_{k-1} = beta_k - Gamma_k' v_k (wave 0)
   if (wv == 0) {
     const int i = lane >> 2, q = lane & 3;
@@ -591,6 +611,7 @@ __device__ __forceinline__ void kkt_solve(Smem<N>& sh, const double (&Si)[4][12]
     }
   }
   __syncthreads();
+  STAMP(7);
   // phase C: w_k = t_k - (S_k^{-1})_{:,X} v_k
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -603,6 +624,7 @@ __device__ __forceinline__ void kkt_solve(Smem<N>& sh, const double (&Si)[4][12]
     }
   }
   __syncthreads();
+  STAMP(8);
 }
 
 // ----------------------------------------------------------------------------
@@ -619,6 +641,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t b = blockIdx.x;
   if (b >= a.batch) return;
+  STAMP_DECL
 
   // slot bookkeeping (rows / columns of this wave's stages)
   int rK[RS], rI[RS], cK[CS], cJ[CS];
@@ -776,6 +799,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 
     if (status == 0) {
       __syncthreads();
+      STAMP(0);
       // ---------------------------------------------------------- Ruiz scaling
       for (int it = 0; it < p.scaling; ++it) {
         double psum = 0.0;
@@ -864,7 +888,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       for (int t = 0; t < CS; ++t)
         if (cV[t]) sh.vn[24 * cK[t] + cJ[t]] = Pb[t] + p.sigma;
       __syncthreads();
+      STAMP(1);
       if (!factor<N>(sh, Si)) status = MPCQ_STATUS_FACTOR_FAILED;
+      STAMP(2);
 
       // ---------------------------------------------------------- ADMM
       double pri_res = 0.0, dua_res = 0.0, eps_pri = 0.0, eps_dua = 0.0;
@@ -939,6 +965,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         for (int t = 0; t < RS; ++t)
           if (rV[t]) sh.vm[44 * rK[t] + rI[t]] = rho[t] * z[t] - y[t];
         __syncthreads();
+        STAMP(3);
         // b = sigma x - q + A' w
 #pragma unroll
         for (int t = 0; t < CS; ++t) {
@@ -948,7 +975,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           sh.vn[24 * cK[t] + cJ[t]] = p.sigma * x[t] + v;
         }
         wave_sync();
-        kkt_solve<N>(sh, Si);
+        kkt_solve<N>(sh, Si KKT_STAMP_PASS);
         // z update, y update (osqp update_z / update_y); x update
 #pragma unroll
         for (int t = 0; t < RS; ++t) {
@@ -967,6 +994,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         can_check = p.check_termination > 0 && (iter % p.check_termination == 0);
         const bool adapt = p.adaptive_rho && p.adaptive_rho_interval > 0 &&
                            (iter % p.adaptive_rho_interval == 0);
+        STAMP(9);
         if (can_check || adapt) {
           __syncthreads();  // vn (w) fully consumed before update_info reuses it
           update_info();
@@ -988,12 +1016,15 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               for (int t = 0; t < CS; ++t)
                 if (cV[t]) sh.vn[24 * cK[t] + cJ[t]] = Pb[t] + p.sigma;
               __syncthreads();
+              STAMP(10);
               if (!factor<N>(sh, Si)) { status = MPCQ_STATUS_FACTOR_FAILED; break; }
+              STAMP(2);
               ++n_upd;
             }
           }
         }
         __syncthreads();
+        STAMP(10);
       }
       it_done = iter > p.max_iter ? p.max_iter : iter;
       if (status == 0) {
@@ -1022,6 +1053,12 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       for (int t = 0; t < RS; ++t)
         if (rV[t]) a.y[b * m + nat_row<N>(rK[t], rI[t])] = nan_out ? NAN : E[t] * y[t] / cscale;
     }
+#ifdef MPCQ_STAMPS
+    STAMP(11);
+    if (tid == 0 && a.stamps) {
+      for (int i = 0; i < 16; ++i) a.stamps[b * 16 + i] = st_acc[i];
+    }
+#endif
     if (tid == 0) {
       if (a.status) a.status[b] = status;
       if (a.iters) a.iters[b] = it_done;

@@ -11,7 +11,9 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmpcq.so")
+# MPCQ_LIB_VARIANT=stamps loads the diagnostic build (per-phase cycle stamps)
+LIB_PATH = os.path.join(HERE, "libmpcq_stamps.so" if os.environ.get("MPCQ_LIB_VARIANT") == "stamps"
+                        else "libmpcq.so")
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 
 # return codes / status / flags / modes (include/mpcq.h)
@@ -31,7 +33,7 @@ MODE_SETUP = 1
 EXPORTS = ("mpcq_abi_version", "mpcq_default_params", "mpcq_dims", "mpcq_pattern",
            "mpcq_supported_horizons", "mpcq_last_error", "mpcq_create", "mpcq_destroy",
            "mpcq_set_stream", "mpcq_last_kernel_ms", "mpcq_formulate_batch",
-           "mpcq_qp_solve_batch", "mpcq_solve_batch")
+           "mpcq_qp_solve_batch", "mpcq_solve_batch", "mpcq_debug_set_stamps")
 
 
 class MpcqError(RuntimeError):
@@ -111,12 +113,13 @@ def lib():
     L.mpcq_last_kernel_ms.argtypes = [vp, dp, dp]
     L.mpcq_formulate_batch.argtypes = [vp, C.c_int64, vp, vp, C.c_int, vp, vp, vp, vp, C.c_uint32]
     L.mpcq_qp_solve_batch.argtypes = [vp, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
-                                      C.c_uint32]
-    L.mpcq_solve_batch.argtypes = [vp, C.c_int64, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp,
+                                      vp, C.c_uint32]
+    L.mpcq_solve_batch.argtypes = [vp, C.c_int64, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp,
                                    C.c_uint32]
+    L.mpcq_debug_set_stamps.argtypes = [vp, vp]
     for name in ("mpcq_dims", "mpcq_pattern", "mpcq_supported_horizons", "mpcq_create",
                  "mpcq_destroy", "mpcq_set_stream", "mpcq_last_kernel_ms", "mpcq_formulate_batch",
-                 "mpcq_qp_solve_batch", "mpcq_solve_batch"):
+                 "mpcq_qp_solve_batch", "mpcq_solve_batch", "mpcq_debug_set_stamps"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

@@ -118,9 +118,10 @@ class Engine:
         st = np.empty(B, np.int32)
         it = np.empty(B, np.int32)
         ro = np.empty(B)
+        info = np.empty((B, 4), np.int32)
         L.check(L.lib().mpcq_qp_solve_batch(self._h, B, _p(Ax), _p(l), _p(u), _p(wx), _p(wy), _p(rho_in),
-                                            _p(x), _p(y), _p(st), _p(it), _p(ro), 0))
-        return dict(x=x, y=y, status=st, iters=it, rho=ro)
+                                            _p(x), _p(y), _p(st), _p(it), _p(ro), _p(info), 0))
+        return dict(x=x, y=y, status=st, iters=it, rho=ro, rho_updates=info[:, 0], polish=info[:, 1])
 
     def solve(self, xref, fsteps, mode: int = L.MODE_UPDATE, warm_x=None, warm_y=None,
               want_x: bool = True, want_y: bool = False):
@@ -132,9 +133,10 @@ class Engine:
         y = np.empty((B, self.m)) if want_y else None
         st = np.empty(B, np.int32)
         it = np.empty(B, np.int32)
+        info = np.empty((B, 4), np.int32)
         L.check(L.lib().mpcq_solve_batch(self._h, B, _p(xref), _p(fsteps), mode, _p(wx), _p(wy), _p(f0),
-                                         _p(x), _p(y), _p(st), _p(it), 0))
-        return dict(f0=f0, x=x, y=y, status=st, iters=it)
+                                         _p(x), _p(y), _p(st), _p(it), _p(info), 0))
+        return dict(f0=f0, x=x, y=y, status=st, iters=it, rho_updates=info[:, 0], polish=info[:, 1])
 
     # ------------------------------------------------------------------ device pointers
     def set_stream(self, stream_handle: int | None):
@@ -142,12 +144,13 @@ class Engine:
 
     def solve_device(self, batch: int, xref_ptr: int, fsteps_ptr: int, f0_ptr: int, status_ptr: int,
                      iters_ptr: int = 0, x_ptr: int = 0, y_ptr: int = 0, mode: int = L.MODE_UPDATE,
-                     warm_x_ptr: int = 0, warm_y_ptr: int = 0, asynchronous: bool = False):
+                     warm_x_ptr: int = 0, warm_y_ptr: int = 0, info_ptr: int = 0,
+                     asynchronous: bool = False):
         flags = L.FLAG_DEVICE_PTRS | (L.FLAG_ASYNC if asynchronous else 0)
         v = lambda q: C.c_void_p(q) if q else None  # noqa: E731
         L.check(L.lib().mpcq_solve_batch(self._h, int(batch), v(xref_ptr), v(fsteps_ptr), mode, v(warm_x_ptr),
                                          v(warm_y_ptr), v(f0_ptr), v(x_ptr), v(y_ptr), v(status_ptr),
-                                         v(iters_ptr), flags))
+                                         v(iters_ptr), v(info_ptr), flags))
 
     def last_kernel_ms(self):
         f = C.c_double()

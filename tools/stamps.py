@@ -1,0 +1,53 @@
+"""Per-phase cycle breakdown of the engine kernel (diagnostic build).
+
+    MPCQ_LIB_VARIANT=stamps python tools/stamps.py [--batch 1024] [--N 16]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "mpc-tsid_amd"))
+os.environ.setdefault("MPCQ_LIB_VARIANT", "stamps")
+
+NAMES = ["prologue", "scaling", "factor", "iter:w", "iter:b+phaseA", "iter:fwd", "iter:phaseB",
+         "iter:bwd", "iter:phaseC", "iter:z/x update", "iter:check+adapt", "epilogue"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--N", type=int, default=16)
+    a = ap.parse_args()
+    import torch
+    import mpcq
+    b = mpcq.synth.make_batch(a.batch, a.N, gaits=("trot",), seed=2000)
+    dev = torch.device("cuda", 0)
+    xr = torch.from_numpy(b["xref"]).to(dev)
+    fs = torch.from_numpy(b["fsteps"]).to(dev)
+    f0 = torch.empty((a.batch, 12), dtype=torch.float64, device=dev)
+    st = torch.empty(a.batch, dtype=torch.int32, device=dev)
+    it = torch.empty(a.batch, dtype=torch.int32, device=dev)
+    stamps = torch.zeros((a.batch, 16), dtype=torch.int64, device=dev)
+    eng = mpcq.Engine(a.N)
+    mpcq.lib().mpcq_debug_set_stamps(eng._h, C.c_void_p(stamps.data_ptr()))
+    eng.solve_device(a.batch, xr.data_ptr(), fs.data_ptr(), f0.data_ptr(), st.data_ptr(), it.data_ptr())
+    torch.cuda.synchronize()
+    S = stamps.cpu().numpy().astype(np.float64)
+    its = it.cpu().numpy()
+    tot = S[:, :12].sum(axis=1)
+    print(f"batch {a.batch} N={a.N}: iters median {np.median(its)} max {its.max()}; "
+          f"kernel ms (event) {eng.last_kernel_ms()[1]:.2f}")
+    print(f"cycles per instance: median {np.median(tot):.3e}; per iteration {np.median(tot / its):.0f}")
+    for i, nm in enumerate(NAMES):
+        share = S[:, i] / tot
+        per_it = S[:, i] / its
+        print(f"  {nm:18s} share {np.median(share) * 100:6.2f}%   cycles/iter {np.median(per_it):9.0f}")
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

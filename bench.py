@@ -110,8 +110,10 @@ def main():
 
     over = dict(polish=2, polish_rounds=8, polish_refine_iter=10) if args.polish else {}
     eng = mpcq.Engine(N, device=local, **over)
-    stream = torch.cuda.current_stream(dev)
-    eng.set_stream(stream.cuda_stream)  # kernel launches on torch's stream -> torch events time them
+    # a dedicated (non-default) HIP stream: the engine launches on it and the
+    # HIP events that time the kernel are recorded on the same stream
+    stream = torch.cuda.Stream(dev)
+    eng.set_stream(stream.cuda_stream)
 
     gather_buf = None
     if args.gather and world > 1:
@@ -123,6 +125,7 @@ def main():
         if args.gather and world > 1:
             dist.gather(f0_d, gather_buf, dst=0)
 
+    torch.cuda.set_stream(stream)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)

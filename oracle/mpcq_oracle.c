@@ -725,7 +725,7 @@ int oracle_qp_solve(const mpcq_params* p, int N, const double* Ax, const double*
     for (int c = 0; c < n; ++c) W->x[c] = p->alpha * W->xt[c] + (1.0 - p->alpha) * W->xp[c];
     for (int r = 0; r < m; ++r) {
       double zr = p->alpha * W->zt[r] + (1.0 - p->alpha) * W->zp[r];
-      double t = zr + W->y[r] / W->rho[r];
+      double t = zr + (1.0 / W->rho[r]) * W->y[r]; /* osqp: rho_inv_vec .* y */
       double zz = t < W->lo[r] ? W->lo[r] : (t > W->hi[r] ? W->hi[r] : t);
       W->y[r] = W->y[r] + W->rho[r] * (zr - zz);
       W->z[r] = zz;

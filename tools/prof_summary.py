@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run (gpurun_out/prof_<tag>) into profiles/.
+
+    python tools/prof_summary.py <tag> [--key c2_N16_B1024]
+
+Writes profiles/<tag>_kernel_stats.csv (the rocprofv3 --kernel-trace --stats
+summary), profiles/<tag>_summary.md (per-launch duration, HBM counters, SQ
+counters) and merges the per-launch HBM traffic into profiles/pmc_traffic.json,
+which bench.py reads for roofline.traffic.
+
+HBM bytes follow MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and
+WRITE_SIZE are KiB per dispatch, collected in separate --pmc passes; on gfx950
+FETCH_SIZE reports half the bytes of a wide coalesced read, so the corrected
+read figure is 2 x FETCH_SIZE (the engine's loads are 8-B-per-lane, for which
+the guide's factor is uncalibrated -- both figures are kept).
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import json
+import os
+import shutil
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counters(path):
+    agg = collections.defaultdict(list)
+    if not os.path.exists(path):
+        return agg
+    for r in csv.DictReader(open(path)):
+        if "engine_kernel" in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return agg
+
+
+def mean(v):
+    return sum(v) / len(v) if v else None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--key", default="c2_N16_B1024")
+    ap.add_argument("--instances", type=int, default=1024)
+    a = ap.parse_args()
+    src = os.path.join(REPO, "gpurun_out", f"prof_{a.tag}")
+    dst = os.path.join(REPO, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{a.tag}_kernel_stats.csv"))
+
+    stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    eng = [r for r in stats if "engine_kernel" in r["Name"]]
+    trace = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
+             if "engine_kernel" in r["Kernel_Name"]]
+    fetch = counters(os.path.join(src, "fetch", "run_counter_collection.csv"))
+    write = counters(os.path.join(src, "write", "run_counter_collection.csv"))
+    sq = counters(os.path.join(src, "sq", "run_counter_collection.csv"))
+
+    fk, wk = mean(fetch.get("FETCH_SIZE", [])), mean(write.get("WRITE_SIZE", []))
+    traffic = None
+    lines = [f"# rocprofv3 summary `{a.tag}` ({a.key})", ""]
+    for r in eng:
+        lines.append(f"- kernel `{r['Name']}`: {r['Calls']} calls, average {float(r['AverageNs']) / 1e6:.3f} ms "
+                     f"(min {float(r['MinNs']) / 1e6:.3f}, max {float(r['MaxNs']) / 1e6:.3f}), "
+                     f"{r['Percentage']} % of GPU time")
+    if trace:
+        t = trace[0]
+        lines.append(f"- launch: grid {t['Grid_Size_X']} threads, workgroup {t['Workgroup_Size_X']}, LDS {t['LDS_Block_Size']} B, "
+                     f"scratch {t['Scratch_Size']} B/lane, arch VGPR {t['VGPR_Count']}, AGPR {t['Accum_VGPR_Count']}, SGPR {t['SGPR_Count']}")
+    if fk is not None and wk is not None:
+        rd_raw, wr = fk * 1024, wk * 1024
+        traffic = 2 * rd_raw + wr
+        lines += ["", "## HBM counters (per launch)", "",
+                  f"- FETCH_SIZE {fk:.1f} KiB -> {rd_raw / 1e6:.3f} MB raw, {2 * rd_raw / 1e6:.3f} MB with the gfx950 x2 correction",
+                  f"- WRITE_SIZE {wk:.1f} KiB -> {wr / 1e6:.3f} MB",
+                  f"- traffic (corrected read + write) {traffic / 1e6:.3f} MB per launch = {traffic / a.instances:.0f} B per instance"]
+    if sq:
+        w = mean(sq.get("SQ_WAVES", [])) or 1.0
+        cyc = mean(sq.get("SQ_WAVE_CYCLES", [])) or 0.0
+        lines += ["", "## SQ counters (per launch; *_CYCLES and WAIT/ACTIVE in quad-cycles)", ""]
+        for name in ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+                     "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU"):
+            v = mean(sq.get(name, []))
+            if v is None:
+                continue
+            extra = f" ({v / w:.4g} per wave)"
+            if name.startswith("SQ_WAIT") or name == "SQ_ACTIVE_INST_ANY":
+                extra += f", {100 * v / cyc:.1f} % of wave cycles" if cyc else ""
+            lines.append(f"- {name}: {v:.4g}{extra}")
+    open(os.path.join(dst, f"{a.tag}_summary.md"), "w").write("\n".join(lines) + "\n")
+    if traffic is not None:
+        path = os.path.join(dst, "pmc_traffic.json")
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            d = {}
+        d[a.key] = {"bytes_per_launch": traffic, "fetch_kib": fk, "write_kib": wk, "tag": a.tag,
+                    "note": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section), separate --pmc passes"}
+        json.dump(d, open(path, "w"), indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,23 @@
+#!/bin/bash
+# rocprofv3 evidence for one bench configuration: kernel-trace stats, then the
+# HBM counters (FETCH_SIZE and WRITE_SIZE in separate passes, as the gfx950 TCC
+# slot budget requires) and one SQ pass.  Counters never share a run with
+# --sys-trace / --runtime-trace.  Every GPU step has its own time limit and the
+# chain stops at the first failure.
+#   bash tools/profile.sh <tag> [bench args...]
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-r01}; shift
+ARGS=${@:---config c2}
+OUT=$R/gpurun_out/prof_$TAG
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+B="python3 $R/bench.py $ARGS --steps 3 --warmup 1 --cpu-sample 0"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $B > $OUT/fetch.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $B > $OUT/write.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU \
+    --output-format csv -d $OUT/sq -o run -- $B > $OUT/sq.log 2>&1
+rc=$?
+echo "profile rc=$rc" >> $OUT/trace.log
+exit $rc

@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=12288,
                     help="instances in the CPU-baseline sample, cycling over the rank-0 batch (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--gather", action="store_true", help="include an RCCL gather of f0 to rank 0 in the timed region")
+    ap.add_argument("--gather", action="store_true", help="include an RCCL all-gather of f0 in the timed region")
     ap.add_argument("--seed", type=int, default=2)
     return ap.parse_args()
 
@@ -88,21 +88,21 @@ def main():
     torch.cuda.set_device(dev)
 
     import mpcq
-    from mpcq import model
+    from mpcq import model, shard
 
     cfg = CONFIGS[args.config]
     N = cfg["N"]
     if args.batch > 0:
-        per = args.batch
+        total = args.batch * world
     elif cfg["per_gpu"]:
-        per = cfg["per_gpu"]
+        total = cfg["per_gpu"] * world
     else:
-        per = -(-cfg["total"] // world)
-    total = per * world
+        total = cfg["total"]
     scaling = "weak" if (cfg["per_gpu"] or args.batch > 0) else "strong"
 
-    # this rank's shard of the synthetic batch (seed = config seed + rank)
-    syn = mpcq.synth.make_batch(per, N, gaits=cfg["gaits"], seed=args.seed * 1000 + rank)
+    # this rank's contiguous shard of the seeded global synthetic batch (mpcq/shard.py)
+    syn = shard.shard_batch(total, world, rank, N, cfg["gaits"], seed=args.seed)
+    per = int(syn["xref"].shape[0])
     xref_d = torch.from_numpy(np.ascontiguousarray(syn["xref"])).to(dev)
     fs_d = torch.from_numpy(np.ascontiguousarray(syn["fsteps"])).to(dev)
     f0_d = torch.empty((per, 12), dtype=torch.float64, device=dev)
@@ -117,15 +117,11 @@ def main():
     stream = torch.cuda.Stream(dev)
     eng.set_stream(stream.cuda_stream)
 
-    gather_buf = None
-    if args.gather and world > 1:
-        gather_buf = [torch.empty_like(f0_d) for _ in range(world)] if rank == 0 else None
-
     def step():
         eng.solve_device(per, xref_d.data_ptr(), fs_d.data_ptr(), f0_d.data_ptr(), st_d.data_ptr(),
                          it_d.data_ptr(), info_ptr=info_d.data_ptr(), asynchronous=True)
         if args.gather and world > 1:
-            dist.gather(f0_d, gather_buf, dst=0)
+            shard.gather_rows(dist, f0_d, total, world, rank)  # forces of every instance on every rank
 
     torch.cuda.set_stream(stream)
     for _ in range(args.warmup):
@@ -148,10 +144,7 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
 
-    tmax = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    wall_max = float(tmax.item())
+    wall_max = shard.max_over_ranks(dist, wall, dev, world)
 
     status = st_d.cpu().numpy()
     iters = it_d.cpu().numpy()

@@ -1,0 +1,199 @@
+"""Drop-in façade of the reference MPC surface over the HIP engine.
+
+Mirrors, name for name, what the reference's control loop touches:
+
+* ``MPC(dt, n_steps, T_gait)``           -- MPC.py:22-82 (one QP per tick) with
+  ``run(k, xref, fsteps)`` (MPC.py:460-514) and the attributes consumers read
+  (``f_applied``, ``x``, ``x_robot``, ``xref``, ``q_next``, ``v_next``,
+  ``q_w``, ``h_ref``, ``P``, ``n_steps``; Logger.py:156,411-418, utils.py:173).
+* ``MPC_Wrapper(dt, n_steps, k_mpc, T_gait, multiprocessing=False)``
+  -- MPC_Wrapper.py:20-112: ``solve(k, fstep_planner)`` returns 0,
+  ``get_latest_result()`` returns ``[0, 0, 8] * 4`` on its first call
+  (MPC_Wrapper.py:64-78), ``run_MPC`` is the compatibility alias named in
+  BASELINE.json (stale caller test_motionless.py:63), plus the batched
+  ``solve_batch(xref[B,12,N+1], fsteps[B,20,13]) -> f0[B,12]``.
+* ``MPC_Virtual(mpc_type, dt_mpc, n_steps, k_mpc, T_gait)`` -- MPC_Virtual.py:20-35.
+
+The tick path is formulate (MPC.update_ML / update_NK, or create_* at k == 0)
+then the OSQP-0.6 solve with the reference's warm start (MPC.py:403-406): x is
+the previous solution shifted by one stage (states: last stage zeroed; forces:
+wrapped, as np.roll does), y and rho carry over from the previous solve as the
+osqp workspace does.  One difference is documented rather than hidden: osqp
+keeps y in its *scaled* coordinates across ``update(Ax=...)`` (which recomputes
+the Ruiz scaling), while the engine carries the unscaled dual and rescales it
+with the new scaling; the two agree whenever the scaling is unchanged.
+
+Errors: the reference crashes on a gait table without a zero-duration
+terminator (MPC.py:636 ``next(...)[0]``) or whose durations do not sum to N
+(MPC.py:627 shape error); here both raise ``ValueError``.  Like the reference,
+``run`` with k > 0 replaces NaN by 0 in the caller's ``fsteps`` (MPC.py:327).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib as L
+from .engine import Engine, pattern
+
+
+def _state_weights(p: L.Params) -> np.ndarray:
+    return np.array([p.state_weights[i] for i in range(12)])
+
+
+class MPC:
+    """One receding-horizon QP per tick on the HIP engine (MPC.py:22-514)."""
+
+    def __init__(self, dt, n_steps, T_gait, device: int = 0, engine: Engine | None = None, **overrides):
+        self.dt = float(dt)
+        self.n_steps = int(n_steps)
+        self.T_gait = T_gait
+        self.engine = engine if engine is not None else Engine(self.n_steps, device=device, dt=self.dt, **overrides)
+        p = self.engine.params
+        self.mass = p.mass
+        self.gI = np.array([p.gI[i] for i in range(9)]).reshape(3, 3)
+        self.mu = p.mu
+        N = self.n_steps
+        self.xref = np.zeros((12, 1 + N))
+        self.x = np.zeros((24 * N,))
+        self.q = np.array([[0.0, 0.0, 0.2027682, 0.0, 0.0, 0.0]]).T
+        self.q_w = self.q.copy()
+        self.v = np.zeros((6, 1))
+        self.h_ref = self.q[2, 0]
+        self.footholds = np.array([p.footholds[i] for i in range(12)]).reshape(3, 4)
+        # P = diag(weights) (MPC.py:236-288), as a CSC matrix like the reference's
+        import scipy.sparse as sp
+        diag = np.concatenate([np.tile(_state_weights(p), N), np.full(12 * N, p.force_weight)])
+        self.P = sp.diags(diag).tocsc()
+        self.Q = np.zeros((24 * N,))
+        self._indptr, self._indices = pattern(N)
+        self.ML = None
+        self.NK = None
+        self.NK_inf = None
+        self.x_robot = np.zeros((12, N))
+        self.f_applied = np.zeros((12,))
+        self.q_next = np.zeros((6, 1))
+        self.v_next = np.zeros((6, 1))
+        self._y = None
+        self._rho = None
+        self.status = None
+        self.iters = None
+
+    def _warm_x(self):
+        """MPC.py:403-406: shift states (zero the last stage) and roll forces."""
+        n_x = 12 * self.n_steps
+        warmx = np.roll(self.x[:n_x], -12).copy()
+        warmx[-12:] = 0
+        warmf = np.roll(self.x[n_x:], -12).copy()
+        return np.hstack((warmx, warmf))
+
+    def run(self, k, xref, fsteps):
+        xref = np.asarray(xref, dtype=np.float64)
+        if xref.shape != (12, self.n_steps + 1):
+            raise ValueError(f"xref must be (12, {self.n_steps + 1}), got {xref.shape}")
+        if np.shape(fsteps) != (20, 13):
+            raise ValueError(f"fsteps must be (20, 13), got {np.shape(fsteps)}")
+        if k > 0:
+            self.q[0:6, 0:1] = xref[0:6, 0:1]
+            self.v[0:6, 0:1] = xref[6:12, 0:1]
+        self.lC = xref[0:3, 0:1]
+        self.xref = xref
+        self.x0 = xref[:, 0:1]
+        mode = L.MODE_SETUP if k == 0 else L.MODE_UPDATE
+        form = self.engine.formulate(xref, fsteps, mode)
+        if form["status"][0] == L.STATUS_BAD_GAIT:
+            raise ValueError("fsteps: gait table needs a zero-duration terminator and durations summing to n_steps")
+        if k > 0:
+            fsteps[np.isnan(fsteps)] = 0.0  # MPC.py:327, the caller's array is mutated
+        import scipy.sparse as sp
+        n, m = 24 * self.n_steps, 44 * self.n_steps
+        self.ML = sp.csc_matrix((form["Ax"][0], self._indices, self._indptr), shape=(m, n))
+        self.NK = form["u"][0].reshape(-1, 1)
+        self.NK_inf = form["l"][0].copy()
+        if k == 0:
+            r = self.engine.qp_solve(form["Ax"], form["l"], form["u"])
+        else:
+            r = self.engine.qp_solve(form["Ax"], form["l"], form["u"], warm_x=self._warm_x(),
+                                     warm_y=self._y, rho=self._rho)
+        self.status = int(r["status"][0])
+        self.iters = int(r["iters"][0])
+        self.x = r["x"][0]
+        self._y = r["y"][0]
+        self._rho = float(r["rho"][0])
+        self.retrieve_result()
+        # world-frame integration (MPC.py:503-510)
+        c_yaw, s_yaw = np.cos(self.q_w[5, 0]), np.sin(self.q_w[5, 0])
+        R = np.array([[c_yaw, -s_yaw], [s_yaw, c_yaw]])
+        self.q_w[0:2, 0:1] += R @ self.q_next[0:2, 0:1]
+        self.q_w[2, 0] = self.q_next[2, 0]
+        self.q_w[3:5, 0] = self.q_next[3:5, 0]
+        self.q_w[5, 0] += self.q_next[5, 0]
+        return 0
+
+    def retrieve_result(self):
+        """MPC.py:432-458."""
+        N = self.n_steps
+        self.x_robot = self.x[:12 * N].reshape((12, N), order="F").copy()
+        self.f_applied = self.x[12 * N:12 * N + 12]
+        self.x_robot += self.xref[:, 1:]
+        self.q_next = self.x_robot[0:6, 0:1]
+        self.v_next = self.x_robot[6:12, 0:1]
+        return 0
+
+
+class MPC_Wrapper:
+    """MPC_Wrapper.py:20-112 over the HIP engine (synchronous)."""
+
+    def __init__(self, dt, n_steps, k_mpc, T_gait, multiprocessing=False, device: int = 0,
+                 engine: Engine | None = None, **overrides):
+        self.f_applied = np.zeros((12,))
+        self.not_first_iter = False
+        self.k_mpc = k_mpc
+        self.multiprocessing = multiprocessing
+        self.mpc = MPC(dt, n_steps, T_gait, device=device, engine=engine, **overrides)
+
+    def solve(self, k, fstep_planner):
+        if self.multiprocessing:
+            # the reference raises here too (MPC_Wrapper.py:48-50)
+            raise RuntimeError("Error: Asynchronous MPC is not up to date")
+        self.run_MPC_synchronous(k, fstep_planner)
+        return 0
+
+    def run_MPC_synchronous(self, k, fstep_planner):
+        self.mpc.run(k / self.k_mpc, fstep_planner.xref, fstep_planner.fsteps)
+        self.f_applied = self.mpc.f_applied
+
+    def run_MPC(self, *args):
+        """Compatibility alias (BASELINE.json's name).  Accepts ``(k, fstep_planner)`` or the stale
+        ``(dt, n_steps, k, T_gait, T_gait/2, joystick, fstep_planner, interface)`` of test_motionless.py:63."""
+        if len(args) == 2:
+            k, planner = args
+        elif len(args) == 8:
+            k, planner = args[2], args[6]
+        else:
+            raise TypeError("run_MPC(k, fstep_planner) or run_MPC(dt, n_steps, k, T_gait, T_gait/2, joystick, "
+                            "fstep_planner, interface)")
+        return self.solve(k, planner)
+
+    def get_latest_result(self):
+        if self.not_first_iter:
+            return self.mpc.f_applied
+        self.not_first_iter = True
+        return np.array([0.0, 0.0, 8.0] * 4)
+
+    def solve_batch(self, xref, fsteps, mode: int = L.MODE_UPDATE, want_x: bool = False):
+        """Batched hot path: B independent ticks (cold-started OSQP solves) -> f0 (B, 12).
+        Returns (f0, info) with info = dict(status, iters, x)."""
+        r = self.mpc.engine.solve(xref, fsteps, mode, want_x=want_x)
+        return r["f0"], dict(status=r["status"], iters=r["iters"], x=r["x"])
+
+
+class MPC_Virtual:
+    """MPC_Virtual.py:20-35: solve / get_latest_result forwarded to the wrapper."""
+
+    def __init__(self, mpc_type, dt_mpc, n_steps, k_mpc, T_gait, device: int = 0, engine: Engine | None = None):
+        if not mpc_type:
+            raise ValueError("only mpc_type=True (the OSQP MPC of MPC.py) exists in the reference")
+        self.solver = MPC_Wrapper(dt_mpc, n_steps, k_mpc, T_gait, multiprocessing=False, device=device,
+                                  engine=engine)
+        self.solve = self.solver.solve
+        self.get_latest_result = self.solver.get_latest_result

@@ -1,0 +1,39 @@
+"""Test-only: an engine stand-in that runs the oracle (CPU), with the Engine
+method signatures the façade uses.  Lets the façade's host logic (warm start,
+dual / rho carry-over, fsteps mutation, first-call forces) be checked without a
+GPU, and gives the GPU façade test its expected values."""
+import numpy as np
+
+
+class OracleEngine:
+    def __init__(self, O, n_steps=16, **overrides):
+        import mpcq
+        self.O = O
+        self.n_steps = n_steps
+        self.params = mpcq.default_params(**overrides)
+        self.oparams = O.default_params(**overrides)
+        self.calls = []
+
+    def formulate(self, xref, fsteps, mode=0):
+        try:
+            Ax, l, u = self.O.formulate(xref, fsteps, mode, self.oparams)
+            st = 0
+        except ValueError:
+            n, m, nnz = self.O.dims(self.n_steps)
+            Ax, l, u, st = np.zeros(nnz), np.zeros(m), np.zeros(m), -11
+        return dict(Ax=Ax[None], l=l[None], u=u[None], status=np.array([st], np.int32))
+
+    def qp_solve(self, Ax, l, u, warm_x=None, warm_y=None, rho=None):
+        self.calls.append(dict(warm_x=None if warm_x is None else np.array(warm_x),
+                               warm_y=None if warm_y is None else np.array(warm_y), rho=rho))
+        r = self.O.qp_solve(self.n_steps, Ax[0], l[0], u[0], self.oparams, warm_x, warm_y, rho)
+        return dict(x=r["x"][None], y=r["y"][None], status=np.array([r["status"]]),
+                    iters=np.array([r["iters"]]), rho=np.array([r["rho"]]))
+
+
+class Planner:
+    """The two attributes MPC_Wrapper.solve reads from a FootstepPlanner (MPC_Wrapper.py:103)."""
+
+    def __init__(self, xref, fsteps):
+        self.xref = np.array(xref)
+        self.fsteps = np.array(fsteps)

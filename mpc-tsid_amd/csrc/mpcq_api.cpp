@@ -71,6 +71,9 @@ int check_params(const mpcq_params* p) {
   if (!(p->force_weight > 0)) return fail(MPCQ_E_INVALID, "force_weight must be > 0");
   for (int i = 0; i < 12; ++i)
     if (!(p->state_weights[i] > 0)) return fail(MPCQ_E_INVALID, "state weights must be > 0");
+  if (p->polish != 0)
+    return fail(MPCQ_E_UNSUPPORTED, "polish is not implemented in the HIP engine yet (polish must be 0, "
+                                    "the OSQP default the reference runs with)");
   return MPCQ_OK;
 }
 

@@ -92,4 +92,6 @@ def test_errors_are_codes_not_crashes(mpcq):
     # bad parameters are rejected before any device work
     bad = mpcq.default_params(alpha=2.5)
     assert lib.mpcq_create(0, 16, C.byref(bad), C.byref(h)) != 0
+    pol = mpcq.default_params(polish=1)  # not in the HIP engine yet: refused, never silently ignored
+    assert lib.mpcq_create(0, 16, C.byref(pol), C.byref(h)) == -4
     lib.mpcq_destroy(None)  # destroying NULL returns a code, never crashes

@@ -1,46 +1,54 @@
 // mpcq_engine.hip — batched convex-MPC QP engine for MI355X (gfx950, CDNA4).
 //
-// One workgroup of N/16 wave64s owns one QP instance for its whole life:
+// One workgroup of N/4 wave64s owns one QP instance for its whole life:
 // formulation (MPC.py:98-378), Ruiz scaling, KKT factorisation and the
 // OSQP-0.6 ADMM iterations run out of registers + LDS.  HBM sees only the
 // compulsory inputs (xref, fsteps) and outputs (f0 / x / y / status).
 //
-// Layout: thread t = 4k + q owns stage k (forces f_k, states X^k := X_{k+1})
-// quarter q: force columns 3q..3q+2 (= foot q), state columns 3q..3q+2, the
-// dynamics rows 3q..3q+2, swing rows 3q..3q+2 and the five friction rows of
-// foot q.  Its ADMM vectors (x, z, y, bounds, scaling) live in registers, as
-// do rows 3q..3q+2 of the two 12x12 inverses below.
+// Lane layout: a stage k is one 16-lane DPP row (so a wave holds 4 stages);
+// lane s = 4f + c of row k is foot f, component c.  Lanes c < 3 own the
+// column pair (force f_k[3f+c], state X_{k+1}[3f+c]) and three rows: the
+// dynamics row 3f+c, the swing row 3f+c and friction row c of foot f; lane
+// c = 3 owns friction rows 3 and 4 of foot f (its column work is a discarded
+// shadow of lane c = 2).  Stage-wide vectors move by DPP row_newbcast,
+// foot-wide ones by quad_perm; only stage-to-stage hand-offs go through LDS.
 //
 // KKT solve (P + sigma I + A' R A) w = b.  In stage order the matrix is block
 // tridiagonal; the forces only couple inside a stage, so they are eliminated
-// first (all stages in parallel, 12x12 per stage, F_k = K_ff,k^{-1} held by
-// the stage's quad), which leaves a block-tridiagonal system in the states
-// with 12x12 blocks:
-//   D_k = K_XX,k - diag(Xd) Q_k diag(Xd) - diag(Hd_{k+1}) Q_{k+1} diag(Hd_{k+1})
-//   L_k = C_X,k  - diag(Xd) Q_k diag(Hd_k)          Q_k = W_k' F_k W_k  (6x6)
-// (W_k = B_k' diag(rho) on the velocity rows, the only rows where forces and
-// states meet).  Block LDL': S_k = D_k - G_k L_k', G_k = L_k S_{k-1}^{-1}.
-// Per ADMM iteration:
-//   u = F b_f, beta = rho B u        (parallel)       bt_X = b_X - K_Xf u - ...
-//   y_k = bt_k - G_k y_{k-1}          (sequential, 12x12, wave 0, 48 lanes)
-//   w_k = S_k^{-1} y_k                (parallel)
-//   X_k = w_k - G_{k+1}' X_{k+1}      (sequential)
-//   f_k = F_k (b_f - W_k gamma_k)     (parallel)
-// Everything else (A x, A' y, projections, residuals) is per stage.
+// first (every stage in parallel: F_k = K_ff,k^{-1}, one row per lane), which
+// leaves a block-tridiagonal system in the states with 12x12 blocks
+//   D_k = K_XX,k - Xd Q_k Xd - Hd_{k+1} Q_{k+1} Hd_{k+1},   Q_k = W_k' F_k W_k (6x6)
+//   L_k = C_X,k  - Xd Q_k Hd_k                              (W_k = R B_k on rows 6..11)
+// factored two-ended ("twisted"): top-down for stages < m, bottom-up for
+// stages > m, meeting at m = N/2, so each substitution sweep is N/2 steps deep:
+//   y_k = b_k - G_k y_{k-1}   (k < m)      v_k = b_k - H_k v_{k+1}   (k > m)
+//   x_m = M^{-1}(y_m + v_m - b_m)
+//   x_k = S_k^{-1} y_k - G_{k+1}' x_{k+1}  x_k = U_k^{-1} v_k - H_{k-1}' x_{k-1}
+// The two sweeps run at once in rows 0 and 1 of wave 0 (one instruction
+// stream), reading G / H from LDS; S^{-1}, U^{-1}, M^{-1} rows stay in the
+// stage lanes' registers.
 #include <math.h>
+
+#include <utility>
 
 #include "mpcq_internal.h"
 
 namespace mpcq {
 namespace {
 
+// LDS views used by the loops.  Reads of loop-invariant data (the scaled A,
+// the sweep matrices) go through these pointers, which the loops launder with
+// an empty asm so the compiler re-reads LDS instead of hoisting dozens of
+// invariant values into registers.
+typedef __attribute__((address_space(3))) const double lds_cd;
+
 constexpr double kInf = 1e30;  // OSQP_INFTY
 constexpr double kMinScaling = 1e-4, kMaxScaling = 1e4;
 constexpr double kRhoMin = 1e-6, kRhoMax = 1e6, kRhoEq = 1e3, kRhoTol = 1e-4;
 constexpr double kDivTol = 1e-30;
 
-// constraint classes -> rho (OSQP set_rho_vec; polish uses 3 / 4)
-enum : int { RC_LOOSE = 0, RC_INEQ = 1, RC_EQ = 2, RC_POL_ACT = 3, RC_POL_OFF = 4 };
+// constraint classes (OSQP set_rho_vec)
+enum : unsigned { RC_LOOSE = 0, RC_INEQ = 1, RC_EQ = 2 };
 
 #ifdef MPCQ_STAMPS
 #define STAMP_DECL uint64_t st_acc[16] = {}; uint64_t st_last = __builtin_amdgcn_s_memtime();
@@ -53,57 +61,70 @@ enum : int { RC_LOOSE = 0, RC_INEQ = 1, RC_EQ = 2, RC_POL_ACT = 3, RC_POL_OFF = 
 // ---------------------------------------------------------------------------
 // CSC offsets of MPC.create_ML's pattern (see mpcq_pattern in mpcq_api.cpp).
 template <int N>
-__device__ __forceinline__ int XO(int k, int i) {  // state column X^k[i] (= X_{k+1}[i])
+__device__ __forceinline__ int XO(int k, int i) {  // state column X_{k+1}[i]
   return (k < N - 1) ? 30 * k + (i < 6 ? 2 * i : 12 + 3 * (i - 6)) : 30 * (N - 1) + i;
 }
 template <int N>
 __device__ __forceinline__ int FO(int k, int f, int c) {  // force column f_k[3f+c]
   return 30 * N - 18 + 96 * k + 24 * f + 7 * c;
 }
+// lane (within the stage row) that owns force / state index psi = 3f + c
+__host__ __device__ constexpr int LN(int psi) { return 4 * (psi / 3) + psi % 3; }
 
 // ---------------------------------------------------------------------------
 // cross-lane helpers
 
 __device__ __forceinline__ void wave_sync() {
-  // LDS is processed in order per wave, so a wave-wide hand-off through LDS
-  // needs no hardware barrier; the asm memory clobber stops the compiler from
-  // moving (or hoisting out of loops) LDS accesses across this point.
+  // LDS is processed in order per wave, so a hand-off inside one wave needs no
+  // hardware barrier; the asm memory clobber stops the compiler from moving
+  // LDS accesses across this point.
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-template <int NW>
-__device__ __forceinline__ void sync_all() {
-  if constexpr (NW == 1) wave_sync();
-  else __syncthreads();
-}
+__device__ __forceinline__ void sync_all() { __syncthreads(); }
 
 template <int CTRL>
 __device__ __forceinline__ double dppd(double v) {
-  const long long bits = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_mov_dpp((int)bits, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(bits >> 32), CTRL, 0xF, 0xF, false);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+  // one v_mov_b64_dpp for row_newbcast (DPP64); other controls split in two.
+  // Every lane of every row is active wherever these run, so no "old" value.
+  return __longlong_as_double(__builtin_amdgcn_mov_dpp(__double_as_longlong(v), CTRL, 0xF, 0xF, false));
 }
-// quad_perm controls
-constexpr int QX1 = 0xB1, QX2 = 0x4E;
+// broadcast lane J of each 16-lane row (DPP row_newbcast, gfx90a+)
 template <int J>
-__device__ __forceinline__ double qbcast(double v) { return dppd<85 * J>(v); }
-__device__ __forceinline__ double quad_sum(double v) {
-  v += dppd<QX1>(v);
-  v += dppd<QX2>(v);
-  return v;
+__device__ __forceinline__ double rbc(double v) { return dppd<0x150 + J>(v); }
+// broadcast lane J of each quad (quad_perm J,J,J,J)
+template <int J>
+__device__ __forceinline__ double qbc(double v) { return dppd<85 * J>(v); }
+
+template <int... J>
+__device__ __forceinline__ void gather_seq(double v, double (&all)[12], std::integer_sequence<int, J...>) {
+  ((all[J] = rbc<LN(J)>(v)), ...);
 }
-// the stage's 12-vector from the 3 entries each quad lane holds (all lanes active)
-__device__ __forceinline__ void quad_gather12(const double (&own)[3], double (&all)[12]) {
-#pragma unroll
-  for (int e = 0; e < 3; ++e) {
-    all[0 + e] = qbcast<0>(own[e]);
-    all[3 + e] = qbcast<1>(own[e]);
-    all[6 + e] = qbcast<2>(own[e]);
-    all[9 + e] = qbcast<3>(own[e]);
-  }
+// the stage's 12-vector from the column lanes
+__device__ __forceinline__ void gather12(double v, double (&all)[12]) {
+  gather_seq(v, all, std::make_integer_sequence<int, 12>{});
+}
+// sum_j M[j * stride] * v_j with v_j broadcast from lane j of the row (three chains for ILP)
+template <int... J>
+__device__ __forceinline__ double dotb_seq(lds_cd* M, int stride, double v, std::integer_sequence<int, J...>) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  (((J % 3 == 0 ? a0 : (J % 3 == 1 ? a1 : a2)) += M[J * stride] * rbc<J>(v)), ...);
+  return (a0 + a1) + a2;
+}
+__device__ __forceinline__ double dotb12(lds_cd* M, int stride, double v) {
+  return dotb_seq(M, stride, v, std::make_integer_sequence<int, 12>{});
+}
+template <int... J>
+__device__ __forceinline__ double dotr_seq(const double (&g)[12], double v, std::integer_sequence<int, J...>) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  (((J % 3 == 0 ? a0 : (J % 3 == 1 ? a1 : a2)) += g[J] * rbc<J>(v)), ...);
+  return (a0 + a1) + a2;
+}
+// sum_j g_j * v_j, v_j broadcast from lane j of the row
+__device__ __forceinline__ double dotr12(const double (&g)[12], double v) {
+  return dotr_seq(g, v, std::make_integer_sequence<int, 12>{});
 }
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
@@ -114,6 +135,42 @@ __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
+}
+// a wave-uniform double kept in SGPRs
+__device__ __forceinline__ double uni(double v) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readfirstlane((int)bits);
+  const int hi = __builtin_amdgcn_readfirstlane((int)(bits >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double sel3(int i, double a0, double a1, double a2) {
+  return i == 0 ? a0 : (i == 1 ? a1 : a2);
+}
+
+// Gauss-Jordan inverse of a 12x12 SPD matrix held one row per column lane
+// (row psi in lane LN(psi)); pivots broadcast by row_newbcast, no pivoting.
+template <int PV>
+__device__ __forceinline__ void gj_step(double (&R)[12], int me, bool& ok) {
+  const double d = rbc<LN(PV)>(R[PV]);
+  if (!(d > 0.0)) ok = false;
+  const double id = 1.0 / d;
+  const double mrp = R[PV];
+  const bool isp = me == PV;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    const double pj = (j == PV) ? d : rbc<LN(PV)>(R[j]);
+    double v;
+    if (isp) v = (j == PV) ? id : pj * id;
+    else v = (j == PV) ? -mrp * id : R[j] - mrp * pj * id;
+    R[j] = v;
+  }
+}
+template <int... P>
+__device__ __forceinline__ void gj_seq(double (&R)[12], int me, bool& ok, std::integer_sequence<int, P...>) {
+  (gj_step<P>(R, me, ok), ...);
+}
+__device__ __forceinline__ void gj12(double (&R)[12], int me, bool& ok) {
+  gj_seq(R, me, ok, std::make_integer_sequence<int, 12>{});
 }
 
 // ---------------------------------------------------------------------------
@@ -134,7 +191,7 @@ __device__ __forceinline__ void inv3(const double* M, double* R) {
 // B rows 9..11 = dt inv(Rz(yaw) gI) [lever]x (MPC.py:339-345), swing flag S
 // (MPC.py:628), friction-cone coefficients (MPC.py:136-148).
 __device__ __forceinline__ void form_foot(const mpcq_params& p, double yaw, double l0, double l1, double l2,
-                          double swing, double* out) {
+                                          double swing, double* out) {
   const double cy = cos(yaw), sy = sin(yaw);
   const double R[9] = {cy, -sy, 0.0, sy, cy, 0.0, 0.0, 0.0, 1.0};
   double M[9], Mi[9];
@@ -189,69 +246,38 @@ __device__ __forceinline__ double dyn_bound(const mpcq_params& p, const double* 
 }
 
 // ---------------------------------------------------------------------------
-// Shared memory of one instance (N=16: 40.8 KB -> 4 instances per CU).
+// Shared memory of one instance (N=16: 40.4 KB -> 4 instances per CU;
+// N=32: 80.2 KB -> 2).
 
 template <int N>
 struct Smem {
   double Ab[126 * N - 18];  // scaled constraint values, CSC order
-  double Gm[N][144];        // G_k (12x12 row-major); during factorisation Q_k [0,36) and
-                            // P+sigma of the states [36,48); in the prologue xref/fsteps/gait
+  // GH[0] = M^{-1}, GH[k] = G_k (1 <= k <= m), GH[k] = H_{k-1} (k > m), row-major.
+  // During the factorisation slot k holds Q_k [0,36), F_k W_k [36,108) and the
+  // dynamics-row rho of stage k [108,120); during scaling the row factors; in
+  // the prologue xref / fsteps / the gait walk.
+  double GH[N][144];
   union {
     struct {
-      double bd[N][12];  // dynamics-row exchange
-      double be[N][8];   // beta exchange
-      double ws[N][12];  // bt -> y (forward recurrence)
-      double xs[N][12];  // w -> X (backward recurrence)
+      double xw[N][12];      // dynamics-row w (A'w), then bt (sweeps' right-hand side)
+      double be[N][6];       // beta = R B u (velocity rows)
+      double yv[N][12];      // sweep outputs y / v, then w = S^{-1} y in place
+      double xs[N + 1][12];  // X_k (xs[k+1] = X_{k+1}, stage k's states)
     } it;
     struct {
-      double Lm[144], Sp[144], Gt[144], Dm[144];
+      double St[144], Sb[144], Lt[144], Lb[144];  // sweep hand-offs of the factorisation
     } fa;
   } u;
-  unsigned char rc[44 * N];  // constraint class per row (stage ordered)
+  double red[12 * (N / 4) + 32];  // per-wave partial reductions; [12 NW, +32) sweep meeting point
   int flag[4];
 };
 
-// prologue aliases inside Gm
+// prologue aliases inside GH
 template <int N>
 struct Prologue {
-  static constexpr int XR = 0;                 // xref, 12(N+1) doubles
-  static constexpr int FS = 12 * (N + 1);      // fsteps, 260 doubles
-  static constexpr int INTS = FS + 260;        // phase_of_stage[N], contact[20][4] as ints
-};
-
-// ---------------------------------------------------------------------------
-// scaled-A accessors (stage k)
-template <int N>
-struct AV {
-  const double* Ab;
-  // dynamics row i (6..11) of stage k on force column a = 3f + c
-  __device__ __forceinline__ double B(int k, int i, int f, int c) const {
-    if (i <= 8) return (c == i - 6) ? Ab[FO<N>(k, f, c)] : 0.0;
-    return Ab[FO<N>(k, f, c) + i - 8];
-  }
-  __device__ __forceinline__ double Xd(int k, int i) const { return Ab[XO<N>(k, i)]; }
-  // dynamics row i of stage k on X^{k-1}[i] (k >= 1)
-  __device__ __forceinline__ double Hd(int k, int i) const {
-    return Ab[XO<N>(k - 1, i) + (i < 6 ? 1 : 2)];
-  }
-  // dynamics row i (< 6) of stage k on X^{k-1}[i+6] (k >= 1)
-  __device__ __forceinline__ double H6(int k, int i) const { return Ab[XO<N>(k - 1, i + 6) + 1]; }
-  __device__ __forceinline__ double Sw(int k, int f, int c) const { return Ab[FO<N>(k, f, c) + 4]; }
-  // friction row 5f+t on component c (0 when absent)
-  __device__ __forceinline__ double Fr(int k, int f, int t, int c) const {
-    int off = -1;
-    if (c == 0 && t < 2) off = 5 + t;
-    else if (c == 1 && (t == 2 || t == 3)) off = 5 + (t - 2);
-    else if (c == 2) off = 5 + t;
-    return off >= 0 ? Ab[FO<N>(k, f, c) + off] : 0.0;
-  }
-};
-
-struct Rho {
-  double v[5];
-  __device__ __forceinline__ double operator()(int cls) const {
-    return cls == RC_INEQ ? v[1] : (cls == RC_EQ ? v[2] : (cls == RC_LOOSE ? v[0] : (cls == RC_POL_ACT ? v[3] : v[4])));
-  }
+  static constexpr int XR = 0;             // xref, 12(N+1) doubles
+  static constexpr int FS = 12 * (N + 1);  // fsteps, 260 doubles
+  static constexpr int INTS = FS + 260;    // phase_of_stage[N], contact[20][4] as ints
 };
 
 // ---------------------------------------------------------------------------
@@ -259,55 +285,96 @@ struct Rho {
 // !FUSED: solve the given (Ax, l, u).  SOLVE=false: formulation only.
 
 template <int N, bool FUSED, bool SOLVE>
-__global__ __launch_bounds__(64 * (N / 16), 1) void engine_kernel(mpcq_params p, LaunchArgs a) {
-  constexpr int NW = N / 16, T = 64 * NW, n = 24 * N, m = 44 * N, nnz = 126 * N - 18;
+__global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, LaunchArgs a) {
+  constexpr int NW = N / 4, T = 16 * N, n = 24 * N, m = 44 * N, nnz = 126 * N - 18, MID = N / 2;
+  constexpr int RMID = 12 * NW;  // sweep meeting point inside red[]
   __shared__ Smem<N> sh;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int k = t >> 2, q = t & 3;
+  const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
+  // lane coordinates; the loops launder them (see launder()) so that the
+  // compiler recomputes the many LDS offsets derived from them instead of
+  // hoisting each one into a register of its own
+  int k = t >> 4, s = t & 15, f = s >> 2, c = s & 3;
+  const bool cl = c < 3;          // column lane (c == 3: friction rows 3, 4 only)
+  int cc = cl ? c : 2;            // column component; c == 3 shadows c == 2
+  int ph = 3 * f + cc;            // own force / state index in the stage
   const int64_t b = blockIdx.x;
   if (b >= a.batch) return;
   STAMP_DECL
-  const AV<N> A{sh.Ab};
-  double* const gm0 = &sh.Gm[0][0];
+  lds_cd* Ab = (lds_cd*)sh.Ab;
+  lds_cd* GHr = (lds_cd*)&sh.GH[0][0];
+  double* const gh0 = &sh.GH[0][0];
+  int fo = FO<N>(k, f, cc), xo = XO<N>(k, ph);  // own force / state column in Ab
+  int cr = t >> 4;                  // sweep row (wave 0): 0 top-down, 1 bottom-up
+  int rr_ = s < 12 ? s : 11;        // sweep lane's state index
+  auto launder = [&]() __attribute__((always_inline)) {
+    asm volatile("" : "+v"(Ab), "+v"(GHr), "+v"(k), "+v"(f), "+v"(c), "+v"(cc), "+v"(ph), "+v"(fo), "+v"(xo),
+                 "+v"(cr), "+v"(rr_));
+  };
+  (void)lane;
 
-  // own rows: j < 3 dyn 3q+j, j < 6 swing 3q+j-3, else friction 5q+j-6 (stage-local index)
-  auto row_i = [&](int j) __attribute__((always_inline)) {
-    return j < 3 ? 3 * q + j : (j < 6 ? 12 + 3 * q + (j - 3) : 24 + 5 * q + (j - 6));
+  // ---- scaled-A accessors ---------------------------------------------------
+  auto Xd = [&](int kk, int i) __attribute__((always_inline)) { return Ab[XO<N>(kk, i)]; };
+  // dynamics row i of stage kk on X_kk[i] / on X_kk[i+6] (i < 6), kk >= 1
+  // (loads stay in bounds for kk == 0 / i >= 6; callers mask those values)
+  auto Hd = [&](int kk, int i) __attribute__((always_inline)) {
+    return Ab[XO<N>(kk > 0 ? kk - 1 : 0, i) + (i < 6 ? 1 : 2)];
   };
-  auto nat_row = [&](int j) __attribute__((always_inline)) {
-    return j < 3 ? 12 * k + 3 * q + j
-                 : (j < 6 ? 12 * N + 12 * k + 3 * q + (j - 3) : 24 * N + 20 * k + 5 * q + (j - 6));
+  auto H6 = [&](int kk, int i) __attribute__((always_inline)) {
+    return Ab[XO<N>(kk > 0 ? kk - 1 : 0, i < 6 ? i + 6 : 11) + 1];
   };
-  // own cols: j < 3 force 3q+j, else state 3q+j-3
-  auto nat_col = [&](int j) __attribute__((always_inline)) {
-    return j < 3 ? 12 * N + 12 * k + 3 * q + j : 12 * k + 3 * q + (j - 3);
+  // coefficient of force psi = 3fp + cp on dynamics row r (6..11) of stage kk
+  auto Bc = [&](int kk, int r, int fp, int cp) __attribute__((always_inline)) -> double {
+    const bool nz = r >= 9 || (r >= 6 && cp == r - 6);
+    const double v = Ab[FO<N>(kk, fp, cp) + (r >= 9 ? r - 8 : 0)];
+    return nz ? v : 0.0;
   };
-  // P diagonal of own column j (MPC.py:255-275)
-  auto P0 = [&](int j) __attribute__((always_inline)) -> double {
-    if (j < 3) return p.force_weight;
-    const int e = j - 3;
-    return q == 0 ? p.state_weights[e]
-                  : (q == 1 ? p.state_weights[3 + e] : (q == 2 ? p.state_weights[6 + e] : p.state_weights[9 + e]));
+  // coefficient of force component cp of foot fp on friction row t of that foot
+  auto Frc = [&](int kk, int fp, int t_, int cp) __attribute__((always_inline)) -> double {
+    const double v = Ab[FO<N>(kk, fp, cp) + (cp == 2 ? 5 + t_ : 5 + (t_ & 1))];
+    return (cp == 2 || (t_ < 4 && (t_ >> 1) == cp)) ? v : 0.0;
+  };
+  // friction row t of foot f at stage k applied to the foot's forces (g0, g1, g2)
+  auto fric_row = [&](int t_, double g0, double g1, double g2) __attribute__((always_inline)) {
+    const int ta = t_ < 4 ? t_ : 0;
+    const double cb = Ab[FO<N>(k, f, 2) + 5 + t_];
+    const double ca = Ab[FO<N>(k, f, ta >> 1) + 5 + (ta & 1)];
+    const double v = cb * g2;
+    return t_ < 4 ? v + ca * ((ta >> 1) == 0 ? g0 : g1) : v;
   };
 
-  // Bounds.  FUSED: dynamics rows keep one value (l = u, MPC.py:410); swing rows
-  // are 0 = 0; friction rows u = 0, l = -inf (-OSQP_INFTY) or -fz_max.  !FUSED:
-  // the caller's l / u for every own row.
-  double bnd[3];
-  double lo_g[FUSED ? 1 : 11], hi_g[FUSED ? 1 : 11];
+  // own rows: slot 0 dyn(k, ph) | fric t=3; slot 1 swing(k, ph) | fric t=4; slot 2 fric t=c | none
+  auto nat_row = [&](int slot) __attribute__((always_inline)) -> int {
+    if (slot == 0) return cl ? 12 * k + ph : 24 * N + 20 * k + 5 * f + 3;
+    if (slot == 1) return cl ? 12 * N + 12 * k + ph : 24 * N + 20 * k + 5 * f + 4;
+    return cl ? 24 * N + 20 * k + 5 * f + c : -1;
+  };
+  const int colF = 12 * N + 12 * k + ph, colX = 12 * k + ph;
+
+  // P diagonal of the own columns (MPC.py:255-275)
+  const double P0f = p.force_weight;
+  double P0X = p.state_weights[0];
+#pragma unroll
+  for (int e = 1; e < 12; ++e)
+    if (ph == e) P0X = p.state_weights[e];
+
+  // Bounds.  FUSED: the dynamics row keeps one value (l = u, MPC.py:410); swing
+  // rows are 0 = 0; friction rows u = 0, l = -inf (-OSQP_INFTY) or -fz_max.
+  // !FUSED: the caller's l / u for every own row.
+  double bnd = 0.0;
+  double lo_g[FUSED ? 1 : 3], hi_g[FUSED ? 1 : 3];
   if (t == 0) { sh.flag[0] = 0; sh.flag[1] = 0; sh.flag[2] = 0; sh.flag[3] = 0; }
 
   // ---------------------------------------------------------------- prologue
   if (FUSED || !SOLVE) {
-    double* xr = gm0 + Prologue<N>::XR;
-    double* fs = gm0 + Prologue<N>::FS;
-    int* pos_ = (int*)(gm0 + Prologue<N>::INTS);  // phase_of_stage[N]
+    double* xr = gh0 + Prologue<N>::XR;
+    double* fs = gh0 + Prologue<N>::FS;
+    int* pos_ = (int*)(gh0 + Prologue<N>::INTS);  // phase_of_stage[N]
     int* con_ = pos_ + N;                         // contact[20][4]
     const double* gx = a.xref + b * 12 * (N + 1);
     const double* gf = a.fsteps + b * 260;
     for (int e = t; e < 12 * (N + 1); e += T) xr[e] = gx[e];
     for (int e = t; e < 260; e += T) fs[e] = gf[e];
-    sync_all<NW>();
+    sync_all();
     if (t == 0) {  // construct_gait + phase walk (MPC.py:635-652, 336-352, 626-631)
       int idx = -1;
       for (int j = 0; j < 20; ++j)
@@ -318,28 +385,29 @@ __global__ __launch_bounds__(64 * (N / 16), 1) void engine_kernel(mpcq_params p,
         if (!(fabs(d) < 1e6)) { bad = 1; break; }
         const int di = (int)d;
         if (di < 0) { bad = 1; break; }
-        for (int f = 0; f < 4; ++f) {
-          const double xv = fs[13 * j + 1 + 3 * f];
-          con_[4 * j + f] = !(isnan(xv) || xv == 0.0);
+        for (int q = 0; q < 4; ++q) {
+          const double xv = fs[13 * j + 1 + 3 * q];
+          con_[4 * j + q] = !(isnan(xv) || xv == 0.0);
         }
-        for (int s = 0; s < di; ++s, ++kk)
+        for (int s_ = 0; s_ < di; ++s_, ++kk)
           if (kk < N) pos_[kk] = j;
       }
       if (kk != N) bad = 1;
       sh.flag[0] = bad ? MPCQ_STATUS_BAD_GAIT : 0;
     }
-    sync_all<NW>();
+    sync_all();
     if (sh.flag[0] == 0) {
-      for (int c = t; c < 12 * N; c += T) {  // state columns: -I / A (MPC.py:107-115)
-        const int kk = c / 12, i = c % 12, xo = XO<N>(kk, i);
+      for (int e = t; e < 12 * N; e += T) {  // state columns: -I / A (MPC.py:107-115)
+        const int kk = e / 12, i = e % 12, xo = XO<N>(kk, i);
         sh.Ab[xo] = -1.0;
         if (kk < N - 1) {
           if (i >= 6) { sh.Ab[xo + 1] = p.dt; sh.Ab[xo + 2] = 1.0; }
           else sh.Ab[xo + 1] = 1.0;
         }
       }
-      {  // foot q of stage k
-        const int j = pos_[k];
+      for (int e = t; e < 4 * N; e += T) {  // foot q of stage kk
+        const int kk = e >> 2, q = e & 3;
+        const int j = pos_[kk];
         double lv[3];
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
@@ -351,28 +419,34 @@ __global__ __launch_bounds__(64 * (N / 16), 1) void engine_kernel(mpcq_params p,
             ft = fs[13 * j + 1 + 3 * q + r];
             if (isnan(ft)) ft = 0.0;  // MPC.py:327
           }
-          lv[r] = ft - xr[r * (N + 1) + k];
+          lv[r] = ft - xr[r * (N + 1) + kk];
         }
-        form_foot(p, xr[5 * (N + 1) + k], lv[0], lv[1], lv[2], 1.0 - (double)con_[4 * j + q],
-                  sh.Ab + FO<N>(k, q, 0));
+        form_foot(p, xr[5 * (N + 1) + kk], lv[0], lv[1], lv[2], 1.0 - (double)con_[4 * j + q],
+                  sh.Ab + FO<N>(kk, q, 0));
       }
-#pragma unroll
-      for (int e = 0; e < 3; ++e) bnd[e] = dyn_bound<N>(p, xr, k, 3 * q + e);
+      bnd = dyn_bound<N>(p, xr, k, ph);
     }
     if (!SOLVE) {
-      sync_all<NW>();
+      sync_all();
       if (t == 0 && a.status) a.status[b] = sh.flag[0];
       if (sh.flag[0] != 0) return;
       double* go = a.Ax_out + b * nnz;
       for (int e = t; e < nnz; e += T) go[e] = sh.Ab[e];
 #pragma unroll
-      for (int j = 0; j < 11; ++j) {
+      for (int slot = 0; slot < 3; ++slot) {
+        const int r = nat_row(slot);
+        if (r < 0) continue;
         double l, u;
-        if (j < 3) { l = bnd[j]; u = bnd[j]; }
-        else if (j < 6) { l = 0.0; u = 0.0; }
-        else { u = 0.0; l = (j == 10) ? -p.fz_max : -INFINITY; }  // l[24N+4::5] = -25 (MPC.py:228)
-        a.l_out[b * m + nat_row(j)] = l;
-        a.u_out[b * m + nat_row(j)] = u;
+        if (cl) {
+          if (slot == 0) { l = bnd; u = bnd; }
+          else if (slot == 1) { l = 0.0; u = 0.0; }
+          else { l = -INFINITY; u = 0.0; }
+        } else {
+          u = 0.0;
+          l = slot == 1 ? -p.fz_max : -INFINITY;  // l[24N+4::5] = -25 (MPC.py:228)
+        }
+        a.l_out[b * m + r] = l;
+        a.u_out[b * m + r] = u;
       }
       return;
     }
@@ -381,540 +455,376 @@ __global__ __launch_bounds__(64 * (N / 16), 1) void engine_kernel(mpcq_params p,
     for (int e = t; e < nnz; e += T) sh.Ab[e] = ga[e];
     if constexpr (!FUSED) {
 #pragma unroll
-      for (int j = 0; j < 11; ++j) {
-        lo_g[j] = a.l[b * m + nat_row(j)];
-        hi_g[j] = a.u[b * m + nat_row(j)];
+      for (int slot = 0; slot < 3; ++slot) {
+        const int r = nat_row(slot);
+        lo_g[slot] = r >= 0 ? a.l[b * m + r] : -kInf;
+        hi_g[slot] = r >= 0 ? a.u[b * m + r] : kInf;
       }
     }
   }
   if constexpr (SOLVE) {
-    sync_all<NW>();
+    sync_all();
     int status = sh.flag[0];
     {  // non-finite data -> NONFINITE (the problem is always feasible otherwise)
       int bad = 0;
       for (int e = t; e < nnz; e += T)
         if (!isfinite(sh.Ab[e])) bad = 1;
       if constexpr (FUSED) {
-#pragma unroll
-        for (int e = 0; e < 3; ++e) if (isnan(bnd[e])) bad = 1;
+        if (cl && isnan(bnd)) bad = 1;
       } else {
 #pragma unroll
-        for (int j = 0; j < 11; ++j) {
+        for (int j = 0; j < 3; ++j) {
           if (isnan(lo_g[j]) || isnan(hi_g[j])) bad = 1;
           lo_g[j] = lo_g[j] < -kInf ? -kInf : lo_g[j];  // python osqp clamps to +-OSQP_INFTY
           hi_g[j] = hi_g[j] > kInf ? kInf : hi_g[j];
         }
       }
       if (status == 0 && bad) atomicOr(&sh.flag[1], 1);
-      sync_all<NW>();
+      sync_all();
       if (status == 0 && sh.flag[1]) status = MPCQ_STATUS_NONFINITE;
     }
 
-    // persistent per-lane state: columns [0,3) forces 3q.., [3,6) states 3q..
-    double x[6], D[6];
-    double z[11], y[11], E[11];
-    double Fr[3][12], Sr[3][12];
-    unsigned int cpack0 = 0u, cpack1 = 0u;  // constraint class per own row, 3 bits each
+    // persistent per-lane state (column values of c == 3 lanes are shadows)
+    double xf = 0.0, xX = 0.0, Df = 1.0, DX = 1.0;
+    double z[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0}, E[3] = {1.0, 1.0, 1.0};
+    double Fr[12], Sr[12];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) { x[j] = 0.0; D[j] = 1.0; }
-#pragma unroll
-    for (int j = 0; j < 11; ++j) { z[j] = 0.0; y[j] = 0.0; E[j] = 1.0; }
-#pragma unroll
-    for (int e = 0; e < 3; ++e)
-#pragma unroll
-      for (int j = 0; j < 12; ++j) { Fr[e][j] = 0.0; Sr[e][j] = 0.0; }
+    for (int j = 0; j < 12; ++j) { Fr[j] = 0.0; Sr[j] = 0.0; }
+    unsigned cls = 0u;
     double cscale = 1.0;
     int it_done = 0, n_upd = 0;
     double rho_s = a.rho_in ? a.rho_in[b] : p.rho;
     rho_s = fmin(fmax(rho_s, kRhoMin), kRhoMax);
-    Rho rho{{kRhoMin, rho_s, kRhoEq * rho_s, 1.0 / p.delta, 0.0}};
-    Rho rinv{{1.0 / kRhoMin, 1.0 / rho_s, 1.0 / (kRhoEq * rho_s), p.delta, 0.0}};
 
-    auto cls = [&](int j) __attribute__((always_inline)) -> int {
-      return (int)((j < 10 ? (cpack0 >> (3 * j)) : (cpack1 >> (3 * (j - 10)))) & 7u);
+    // per-row rho / 1/rho from the row's class and the (uniform) rho values
+    double r_in = 0.0, r_eq = 0.0, ri_in = 0.0, ri_eq = 0.0;
+    auto set_rho = [&]() __attribute__((always_inline)) {
+      r_in = uni(rho_s);
+      r_eq = uni(kRhoEq * rho_s);
+      ri_in = uni(1.0 / r_in);
+      ri_eq = uni(1.0 / r_eq);
     };
-    // scaled bounds of own row j
+    auto rho_of = [&](int j) __attribute__((always_inline)) -> double {
+      const unsigned cj = (cls >> (2 * j)) & 3u;
+      return cj == RC_EQ ? r_eq : (cj == RC_INEQ ? r_in : kRhoMin);
+    };
+    auto rinv_of = [&](int j) __attribute__((always_inline)) -> double {
+      const unsigned cj = (cls >> (2 * j)) & 3u;
+      return cj == RC_EQ ? ri_eq : (cj == RC_INEQ ? ri_in : 1.0 / kRhoMin);
+    };
     auto lo_of = [&](int j) __attribute__((always_inline)) -> double {
       if constexpr (FUSED) {
-        if (j < 3) return bnd[j];
-        if (j < 6) return 0.0;
-        return (j == 10 ? -p.fz_max : -kInf) * E[j];
+        if (j == 0) return cl ? bnd : -kInf * E[0];
+        if (j == 1) return cl ? 0.0 : -p.fz_max * E[1];
+        return cl ? -kInf * E[2] : -kInf;
       } else {
         return lo_g[j];
       }
     };
     auto hi_of = [&](int j) __attribute__((always_inline)) -> double {
       if constexpr (FUSED) {
-        if (j < 3) return bnd[j];
-        return 0.0;
+        if (j == 0) return cl ? bnd : 0.0;
+        if (j == 1) return 0.0;
+        return cl ? 0.0 : kInf;
       } else {
         return hi_g[j];
       }
     };
-    auto Pbar = [&](int j) __attribute__((always_inline)) -> double {  // c D P D
-      return cscale * (D[j] * P0(j) * D[j]);
+
+    // ---- row / column operators --------------------------------------------
+    // A v for own rows from own forces vf (column lanes), own states vX and the
+    // previous stage's states in xs[k]; also returns the force gather.
+    auto row_A = [&](double vf, double vX, double (&out)[3]) __attribute__((always_inline)) {
+      double fall[12];
+      gather12(vf, fall);
+      const double* xp = sh.u.it.xs[k];  // xs[0] is never read unmasked
+      const double hd = Hd(k, ph), h6 = H6(k, ph);
+      const double xa = xp[ph], xb = xp[ph < 6 ? ph + 6 : ph];
+      double dyn = Xd(k, ph) * vX;
+      const double d1 = dyn + hd * xa;
+      const double d2 = d1 + h6 * xb;
+      dyn = k >= 1 ? (ph < 6 ? d2 : d1) : dyn;
+      double bf = 0.0;
+#pragma unroll
+      for (int psi = 0; psi < 12; ++psi) bf += Bc(k, ph, psi / 3, psi % 3) * fall[psi];
+      dyn = ph >= 6 ? dyn + bf : dyn;
+      const double g0 = qbc<0>(vf), g1 = qbc<1>(vf), g2 = qbc<2>(vf);
+      const double swg = Ab[fo + 4] * vf;
+      out[0] = cl ? dyn : fric_row(3, g0, g1, g2);
+      out[1] = cl ? swg : fric_row(4, g0, g1, g2);
+      out[2] = cl ? fric_row(c, g0, g1, g2) : 0.0;
+    };
+    // A' w for the own columns: wo = w of own rows, xw[k+1] = next stage's dynamics w
+    auto col_At = [&](const double (&wo)[3], double& of, double& oX) __attribute__((always_inline)) {
+      const double w6 = rbc<LN(6)>(wo[0]), w7 = rbc<LN(7)>(wo[0]), w8 = rbc<LN(8)>(wo[0]);
+      const double w9 = rbc<LN(9)>(wo[0]), w10 = rbc<LN(10)>(wo[0]), w11 = rbc<LN(11)>(wo[0]);
+      const double wf0 = qbc<0>(wo[2]), wf1 = qbc<1>(wo[2]), wf2 = qbc<2>(wo[2]);
+      const double wf3 = qbc<3>(wo[0]), wf4 = qbc<3>(wo[1]);
+      double sF = Ab[fo] * sel3(cc, w6, w7, w8);
+      sF += Ab[fo + 1] * w9;
+      sF += Ab[fo + 2] * w10;
+      sF += Ab[fo + 3] * w11;
+      sF += Ab[fo + 4] * wo[1];
+      sF += Ab[fo + 5] * (cc == 1 ? wf2 : wf0);
+      sF += Ab[fo + 6] * (cc == 1 ? wf3 : wf1);
+      const double e7 = Ab[fo + 7], e8 = Ab[fo + 8], e9 = Ab[fo + 9];  // friction rows 2..4 (cc == 2)
+      of = cc == 2 ? ((sF + e7 * wf2) + e8 * wf3) + e9 * wf4 : sF;
+      const double* wn = sh.u.it.xw[k < N - 1 ? k + 1 : k];
+      const double sX = Ab[xo] * wo[0];
+      const double x1 = sX + Ab[xo + 1] * wn[ph >= 6 ? ph - 6 : ph];
+      const double x2 = x1 + Ab[xo + 2] * wn[ph];
+      oX = k < N - 1 ? (ph >= 6 ? x2 : x1) : sX;
+    };
+    auto Pbf = [&]() __attribute__((always_inline)) { return cscale * (Df * P0f * Df); };
+    auto PbX = [&]() __attribute__((always_inline)) { return cscale * (DX * P0X * DX); };
+
+    // ---- factorisation --------------------------------------------------------
+    // dynamics-row rho of stage kk (published in GH[kk][108..120) at factor time)
+    auto rdy = [&](int kk, int i) __attribute__((always_inline)) { return GHr[144 * kk + 108 + i]; };
+    auto Qv = [&](int kk, int j1, int j2) __attribute__((always_inline)) { return GHr[144 * kk + 6 * j1 + j2]; };
+    // entry (jr, ic) of L_kk: dynamics rows of stage kk on (X_{kk+1}[jr], X_kk[ic]), kk >= 1
+    auto Lval = [&](int kk, int jr, int ic) __attribute__((always_inline)) -> double {
+      double v = 0.0;
+      if (ic == jr) v = rdy(kk, jr) * Xd(kk, jr) * Hd(kk, jr);
+      if (jr < 6 && ic == jr + 6) v = rdy(kk, jr) * Xd(kk, jr) * H6(kk, jr);
+      if (jr >= 6 && ic >= 6) v -= Xd(kk, jr) * Qv(kk, jr - 6, ic - 6) * Hd(kk, ic);
+      return v;
+    };
+    // row i of D_kk (state block of X_{kk+1})
+    auto Drow = [&](int kk, int i, double diag0, double (&Dr)[12]) __attribute__((always_inline)) {
+      const double Xdi = Xd(kk, i);
+      double dg = diag0 + rdy(kk, i) * Xdi * Xdi;
+      double h1 = 0.0, h6 = 0.0;
+      if (kk < N - 1) {
+        h1 = Hd(kk + 1, i);
+        dg += rdy(kk + 1, i) * h1 * h1;
+        if (i >= 6) { h6 = H6(kk + 1, i - 6); dg += rdy(kk + 1, i - 6) * h6 * h6; }
+      }
+#pragma unroll
+      for (int ci = 0; ci < 12; ++ci) {
+        double v = (ci == i) ? dg : 0.0;
+        if (kk < N - 1) {
+          if (i < 6 && ci == i + 6) v = rdy(kk + 1, i) * h1 * H6(kk + 1, i);
+          if (i >= 6 && ci == i - 6) v = rdy(kk + 1, ci) * Hd(kk + 1, ci) * h6;
+        }
+        if (i >= 6 && ci >= 6) {
+          v -= Xdi * Qv(kk, i - 6, ci - 6) * Xd(kk, ci);
+          if (kk < N - 1) v -= h1 * Qv(kk + 1, i - 6, ci - 6) * Hd(kk + 1, ci);
+        }
+        Dr[ci] = v;
+      }
     };
 
-    // ---- column / row operators on the stage layout ---------------------
-    // A' w for own columns.  wown = w of own rows; dyn-row w of all stages in bd.
-    auto col_At = [&](const double (&wown)[11], double (&out)[6]) __attribute__((always_inline)) {
-      const double* wk = sh.u.it.bd[k];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const int fo = FO<N>(k, q, c);
-        double s = sh.Ab[fo] * wk[6 + c];
-        s += sh.Ab[fo + 1] * wk[9];
-        s += sh.Ab[fo + 2] * wk[10];
-        s += sh.Ab[fo + 3] * wk[11];
-        s += sh.Ab[fo + 4] * wown[3 + c];
-        if (c == 0) { s += sh.Ab[fo + 5] * wown[6]; s += sh.Ab[fo + 6] * wown[7]; }
-        else if (c == 1) { s += sh.Ab[fo + 5] * wown[8]; s += sh.Ab[fo + 6] * wown[9]; }
-        else {
-#pragma unroll
-          for (int tt = 0; tt < 5; ++tt) s += sh.Ab[fo + 5 + tt] * wown[6 + tt];
-        }
-        out[c] = s;
-      }
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        const int i = 3 * q + e, xo = XO<N>(k, i);
-        double s = sh.Ab[xo] * wown[e];
-        if (k < N - 1) {
-          const double* wn = sh.u.it.bd[k + 1];
-          if (i >= 6) { s += sh.Ab[xo + 1] * wn[i - 6]; s += sh.Ab[xo + 2] * wn[i]; }
-          else s += sh.Ab[xo + 1] * wn[i];
-        }
-        out[3 + e] = s;
-      }
-    };
-    // (B f)_{6..11} of the stage from the own force columns (quad sums; all lanes)
-    auto Bf6 = [&](const double (&fown)[3], double (&bf6)[6]) __attribute__((always_inline)) {
-      double pp[6];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) pp[c] = sh.Ab[FO<N>(k, q, c)] * fown[c];
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        double s = 0.0;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) s += sh.Ab[FO<N>(k, q, c) + 1 + r] * fown[c];
-        pp[3 + r] = s;
-      }
-#pragma unroll
-      for (int j = 0; j < 6; ++j) bf6[j] = quad_sum(pp[j]);
-    };
-    // A v for own rows: fown = own forces, vx = own states, previous stage's states in xs[k-1]
-    auto row_A = [&](const double (&fown)[3], const double (&vx)[3], double (&out)[11]) __attribute__((always_inline)) {
-      double bf6[6];
-      Bf6(fown, bf6);
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        const int i = 3 * q + e;
-        double s = 0.0;
-        if (k >= 1) {
-          const double* xp = sh.u.it.xs[k - 1];
-          s += A.Hd(k, i) * xp[i];
-          if (i < 6) s += A.H6(k, i) * xp[i + 6];
-        }
-        s += A.Xd(k, i) * vx[e];
-        if (q == 2) s += bf6[e];
-        else if (q == 3) s += bf6[3 + e];
-        out[e] = s;
-      }
-#pragma unroll
-      for (int c = 0; c < 3; ++c) out[3 + c] = A.Sw(k, q, c) * fown[c];
-      const int b0 = FO<N>(k, q, 0), b1 = FO<N>(k, q, 1), b2 = FO<N>(k, q, 2);
-      out[6] = sh.Ab[b0 + 5] * fown[0] + sh.Ab[b2 + 5] * fown[2];
-      out[7] = sh.Ab[b0 + 6] * fown[0] + sh.Ab[b2 + 6] * fown[2];
-      out[8] = sh.Ab[b1 + 5] * fown[1] + sh.Ab[b2 + 7] * fown[2];
-      out[9] = sh.Ab[b1 + 6] * fown[1] + sh.Ab[b2 + 8] * fown[2];
-      out[10] = sh.Ab[b2 + 9] * fown[2];
-    };
-    // per-row rho of a dynamics row (k', i) from the class table
-    auto rho_dyn = [&](int kk, int i) __attribute__((always_inline)) { return rho((int)sh.rc[44 * kk + i]); };
-
-    // ---- factorisation -----------------------------------------------------
-    // Phase P (every quad, its stage): F = K_ff^{-1}, Q = W' F W.  Phase S (wave
-    // 0, 48 lanes, sequential in k): S_k^{-1}, G_k.
     auto factor = [&](double sigma) __attribute__((always_inline)) -> bool {
       bool ok = true;
+      launder();
+      double* gk = sh.GH[k];
+      if (cl) gk[108 + ph] = rho_of(0);
+      sync_all();
+      // ---- phase P: F_k = K_ff^{-1} (row ph per column lane), F_k W_k, Q_k
       {
-        // K_ff rows 3q+c, built in place in Fr and inverted there
+        double rd6[6];
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-#pragma unroll
-          for (int bb = 0; bb < 12; ++bb) {
-            const int fb = bb / 3, cbb = bb % 3;
-            double v = 0.0;
-#pragma unroll
-            for (int i = 6; i < 12; ++i) {
-              const double ba = A.B(k, i, q, c), bbv = A.B(k, i, fb, cbb);
-              v += rho_dyn(k, i) * ba * bbv;
-            }
-            if (bb == 3 * q + c) {
-              const double sw = A.Sw(k, q, c);
-              v += Pbar(c) + sigma + rho(cls(3 + c)) * sw * sw;
-            }
-            if (fb == q) {
-#pragma unroll
-              for (int tt = 0; tt < 5; ++tt)
-                v += rho(cls(6 + tt)) * A.Fr(k, q, tt, c) * A.Fr(k, q, tt, cbb);
-            }
-            Fr[c][bb] = v;
-          }
-        // Gauss-Jordan inverse inside the quad (SPD, no pivoting)
-#pragma unroll
-        for (int pv = 0; pv < 12; ++pv) {
-          const int pl = pv / 3, pe = pv % 3;
-          double prow[12];
-#pragma unroll
-          for (int j = 0; j < 12; ++j) {
-            const double src = Fr[pe][j];
-            prow[j] = pl == 0 ? qbcast<0>(src) : (pl == 1 ? qbcast<1>(src) : (pl == 2 ? qbcast<2>(src) : qbcast<3>(src)));
-          }
-          const double d = prow[pv];
-          if (!(d > 0.0)) ok = false;
-          const double id = 1.0 / d;
-#pragma unroll
-          for (int e = 0; e < 3; ++e) {
-            const bool isp = (q == pl) && (e == pe);
-            const double mrp = Fr[e][pv];
-#pragma unroll
-            for (int j = 0; j < 12; ++j) {
-              double v;
-              if (isp) v = (j == pv) ? id : prow[j] * id;
-              else v = (j == pv) ? -mrp * id : Fr[e][j] - mrp * prow[j] * id;
-              Fr[e][j] = v;
-            }
-          }
+        for (int j = 0; j < 6; ++j) rd6[j] = gk[114 + j];
+        double rfr[5];
+        {
+          const double r0 = rho_of(0), r1 = rho_of(1), r2 = rho_of(2);
+          rfr[0] = qbc<0>(r2); rfr[1] = qbc<1>(r2); rfr[2] = qbc<2>(r2);
+          rfr[3] = qbc<3>(r0); rfr[4] = qbc<3>(r1);
         }
-        // Q = W' F W (6x6), W[bb][j] = rho_{6+j} B[6+j][bb]; one column of F W at a time
+        const double Bo0 = Ab[fo], Bo1 = Ab[fo + 1], Bo2 = Ab[fo + 2], Bo3 = Ab[fo + 3];
+        const double sw = Ab[fo + 4];
+        const double rsw = rho_of(1);  // swing-row rho (own slot 1)
+        double own_fr[5];
 #pragma unroll
-        for (int jj = 0; jj < 6; ++jj) {
-          double zc[3] = {0.0, 0.0, 0.0};
-          const double rj = rho_dyn(k, 6 + jj);
+        for (int t_ = 0; t_ < 5; ++t_) own_fr[t_] = rfr[t_] * Frc(k, f, t_, cc);
+        const double dgf = Pbf() + sigma + rsw * sw * sw;
 #pragma unroll
-          for (int bb = 0; bb < 12; ++bb) {
-            const double w = rj * A.B(k, 6 + jj, bb / 3, bb % 3);
+        for (int psi = 0; psi < 12; ++psi) {
+          const int fp = psi / 3, cp = psi % 3;
+          double v = (cp == cc) ? rd6[cp] * Bo0 * Ab[FO<N>(k, fp, cp)] : 0.0;
+          v += rd6[3] * Bo1 * Ab[FO<N>(k, fp, cp) + 1];
+          v += rd6[4] * Bo2 * Ab[FO<N>(k, fp, cp) + 2];
+          v += rd6[5] * Bo3 * Ab[FO<N>(k, fp, cp) + 3];
+          if (psi == ph) v += dgf;
+          if (fp == f) {
+            double fr = 0.0;
 #pragma unroll
-            for (int e = 0; e < 3; ++e) zc[e] += Fr[e][bb] * w;
+            for (int t_ = 0; t_ < 5; ++t_) fr += own_fr[t_] * Frc(k, f, t_, cp);
+            v += fr;
           }
-#pragma unroll
-          for (int j = 0; j < 6; ++j) {
-            double s = 0.0;
-#pragma unroll
-            for (int e = 0; e < 3; ++e) s += rho_dyn(k, 6 + j) * A.B(k, 6 + j, q, e) * zc[e];
-            s = quad_sum(s);
-            if (q == 0) sh.Gm[k][6 * j + jj] = s;
-          }
+          Fr[psi] = v;
         }
+        gj12(Fr, ph, ok);
+        // F W (row ph): W[psi][j] = rho_{6+j} B[6+j][psi]
+        double fw[6];
 #pragma unroll
-        for (int e = 0; e < 3; ++e) sh.Gm[k][36 + 3 * q + e] = Pbar(3 + e) + sigma;
+        for (int j = 0; j < 6; ++j) {
+          double acc = 0.0;
+#pragma unroll
+          for (int psi = 0; psi < 12; ++psi) {
+            const double bv = Bc(k, 6 + j, psi / 3, psi % 3);
+            if (j >= 3 || psi % 3 == j) acc += Fr[psi] * (rd6[j] * bv);
+          }
+          fw[j] = acc;
+        }
+        if (cl) {
+#pragma unroll
+          for (int j = 0; j < 6; ++j) gk[36 + 6 * ph + j] = fw[j];
+        }
+        wave_sync();
+        // Q = W' (F W): 36 entries over the row's 16 lanes
+        for (int e = s; e < 36; e += 16) {
+          const int j1 = e / 6, j2 = e % 6;
+          const double r1 = gk[114 + j1];
+          double acc = 0.0;
+#pragma unroll
+          for (int psi = 0; psi < 12; ++psi)
+            acc += (r1 * Bc(k, 6 + j1, psi / 3, psi % 3)) * gk[36 + 6 * psi + j2];
+          gk[e] = acc;
+        }
       }
-      sync_all<NW>();
-      // Phase S
-      const int r = lane >> 2, cb = lane & 3;
-      const bool act = (wv == 0) && lane < 48;
-      double* Lm = sh.u.fa.Lm;
-      double* Sp = sh.u.fa.Sp;
-      double* Gt = sh.u.fa.Gt;
-      for (int kk = 0; kk < N; ++kk) {
-        double mreg[3] = {0.0, 0.0, 0.0};
-        if (wv == 0) {
-          double Dv[3], Lv[3];
-          if (act) {
-            const double xdr = A.Xd(kk, r);
-            const double* Qk = sh.Gm[kk];
-#pragma unroll
-            for (int e = 0; e < 3; ++e) {
-              const int c = 3 * cb + e;
-              double v = 0.0;
-              if (r == c) v = sh.Gm[kk][36 + r] + rho_dyn(kk, r) * xdr * xdr;
-              if (kk < N - 1) {
-                // dynamics rows of stage kk+1 on X^kk (coefficients live in X^kk's columns)
-                const double hr = A.Hd(kk + 1, r);
-                if (r == c) {
-                  v += rho_dyn(kk + 1, r) * hr * hr;
-                  if (r >= 6) { const double h6 = A.H6(kk + 1, r - 6); v += rho_dyn(kk + 1, r - 6) * h6 * h6; }
-                }
-                if (c == r + 6) v += rho_dyn(kk + 1, r) * hr * A.H6(kk + 1, r);
-                if (r == c + 6) v += rho_dyn(kk + 1, c) * A.Hd(kk + 1, c) * A.H6(kk + 1, c);
-              }
-              if (r >= 6 && c >= 6) {
-                v -= xdr * Qk[6 * (r - 6) + (c - 6)] * A.Xd(kk, c);
-                if (kk < N - 1) v -= A.Hd(kk + 1, r) * sh.Gm[kk + 1][6 * (r - 6) + (c - 6)] * A.Hd(kk + 1, c);
-              }
-              Dv[e] = v;
-              double l = 0.0;
-              if (kk >= 1) {
-                if (c == r) l = rho_dyn(kk, r) * xdr * A.Hd(kk, r);
-                else if (c == r + 6 && r < 6) l = rho_dyn(kk, r) * xdr * A.H6(kk, r);
-                if (r >= 6 && c >= 6) l -= xdr * Qk[6 * (r - 6) + (c - 6)] * A.Hd(kk, c);
-              }
-              Lv[e] = l;
+      const double dgX = PbX() + sigma;
+      sync_all();
+      // ---- phase S: two-ended block factorisation of the state system.  Per
+      // step the active row keeps one 12-vector live (its row of S / U / M):
+      // L goes to LDS entry by entry, G / H straight to their GH slot.
+      double* const St = sh.u.fa.St;
+      double* const Sb = sh.u.fa.Sb;
+      double* const Lt = sh.u.fa.Lt;
+      double* const Lb = sh.u.fa.Lb;
+      // Step j < MID: top row k = j (C = L_k against S_{k-1}^{-1}) and bottom row
+      // k = N-1-j > MID (C = L_{k+1}' against U_{k+1}^{-1}) in parallel; step MID:
+      // the meeting row (both couplings).  G_k -> GH[k], H_k -> GH[k+1], M^{-1} -> GH[0].
+#pragma nounroll
+      for (int j = 0; j <= MID; ++j) {
+        launder();
+        const bool mid = j == MID;
+        const bool top = !mid && k == j, bot = !mid && k == N - 1 - j && k > MID, mrow = mid && k == MID;
+        if (top || bot || mrow) {
+          const bool useT = (top && k > 0) || mrow, useB = (bot && k < N - 1) || mrow;
+          double* const Sw = bot ? Sb : St;  // holds the previous inverse, then this row's block
+          double Ro[12];
+          Drow(k, ph, dgX, Ro);  // every read of GH[k], GH[k+1] by this row happens here ...
+          if (cl) {
+#pragma unroll 1
+            for (int ci = 0; ci < 12; ++ci) {
+              if (useT) Lt[12 * ph + ci] = Lval(k, ph, ci);
+              if (useB) Lb[12 * ph + ci] = Lval(k + 1, ci, ph);
             }
           }
-          if (kk >= 1) {
-            if (act) {
+          wave_sync();  // ... and here, so G / H may now overwrite those slots
+          if (cl) {
+#pragma unroll 1
+            for (int ci = 0; ci < 12; ++ci) {
+              if (useT) {
+                double acc = 0.0;
 #pragma unroll
-              for (int e = 0; e < 3; ++e) Lm[12 * r + 3 * cb + e] = Lv[e];
-            }
-            wave_sync();
-            double g[3] = {0.0, 0.0, 0.0};
-            if (act) {
-#pragma unroll
-              for (int tt = 0; tt < 12; ++tt) {
-                const double lrt = Lm[12 * r + tt];
-#pragma unroll
-                for (int e = 0; e < 3; ++e) g[e] += lrt * Sp[12 * tt + 3 * cb + e];
+                for (int jj = 0; jj < 12; ++jj) acc += Lt[12 * ph + jj] * St[12 * jj + ci];
+                sh.GH[k][12 * ph + ci] = acc;  // G_k = L_k S_{k-1}^{-1}
               }
+              if (useB) {
+                double acc = 0.0;
 #pragma unroll
-              for (int e = 0; e < 3; ++e) Gt[12 * r + 3 * cb + e] = g[e];
-            }
-            wave_sync();
-            if (act) {
-#pragma unroll
-              for (int e = 0; e < 3; ++e) {
-                const int c = 3 * cb + e;
-                double s = 0.0;
-#pragma unroll
-                for (int tt = 0; tt < 12; ++tt) s += Gt[12 * r + tt] * Lm[12 * c + tt];
-                mreg[e] = Dv[e] - s;
+                for (int jj = 0; jj < 12; ++jj) acc += Lb[12 * ph + jj] * Sb[12 * jj + ci];
+                sh.GH[k + 1][12 * ph + ci] = acc;  // H_k = L_{k+1}' U_{k+1}^{-1}
               }
             }
-          } else {
-#pragma unroll
-            for (int e = 0; e < 3; ++e) mreg[e] = act ? Dv[e] : 0.0;
           }
-          // Gauss-Jordan inverse of S_kk, entries (r, 3cb..3cb+2), via lane shuffles
+          wave_sync();  // the previous inverse is consumed: Sw takes this row's block
+          if (cl) {
 #pragma unroll
-          for (int pv = 0; pv < 12; ++pv) {
-            const int pl = pv / 3, pe = pv % 3;
-            const double pr0 = __shfl(mreg[0], 4 * pv + cb);
-            const double pr1 = __shfl(mreg[1], 4 * pv + cb);
-            const double pr2 = __shfl(mreg[2], 4 * pv + cb);
-            const double msel = pe == 0 ? mreg[0] : (pe == 1 ? mreg[1] : mreg[2]);
-            const double mcol = __shfl(msel, 4 * r + pl);
-            const double d = __shfl(msel, 4 * pv + pl);
-            if (!(d > 0.0)) ok = false;
-            const double id = 1.0 / d;
-            const double prow[3] = {pr0, pr1, pr2};
+            for (int ci = 0; ci < 12; ++ci) Sw[12 * ph + ci] = Ro[ci];
+#pragma unroll 1
+            for (int ci = 0; ci < 12; ++ci) {
+              double acc = Sw[12 * ph + ci];
+              if (useT) {
 #pragma unroll
-            for (int e = 0; e < 3; ++e) {
-              const int c = 3 * cb + e;
-              double v;
-              if (r == pv) v = (c == pv) ? id : prow[e] * id;
-              else v = (c == pv) ? -mcol * id : mreg[e] - mcol * prow[e] * id;
-              mreg[e] = v;
+                for (int jj = 0; jj < 12; ++jj) acc -= sh.GH[k][12 * ph + jj] * Lt[12 * ci + jj];
+              }
+              if (useB) {
+#pragma unroll
+                for (int jj = 0; jj < 12; ++jj) acc -= sh.GH[k + 1][12 * ph + jj] * Lb[12 * ci + jj];
+              }
+              Sw[12 * ph + ci] = acc;
             }
           }
-          if (act) {
+          wave_sync();
 #pragma unroll
-            for (int e = 0; e < 3; ++e) Sp[12 * r + 3 * cb + e] = mreg[e];
+          for (int ci = 0; ci < 12; ++ci) Ro[ci] = Sw[12 * ph + ci];
+          gj12(Ro, ph, ok);
+#pragma unroll
+          for (int ci = 0; ci < 12; ++ci) Sr[ci] = Ro[ci];
+          wave_sync();
+          if (cl) {
+            double* dst = mrow ? &sh.GH[0][0] : Sw;
+#pragma unroll
+            for (int ci = 0; ci < 12; ++ci) dst[12 * ph + ci] = Ro[ci];
           }
         }
-        sync_all<NW>();
-        // G_kk -> Gm[kk] (the Q / P entries of stage kk are no longer needed)
-        if (act) {
-#pragma unroll
-          for (int e = 0; e < 3; ++e) sh.Gm[kk][12 * r + 3 * cb + e] = (kk >= 1) ? Gt[12 * r + 3 * cb + e] : 0.0;
-        }
-        if (k == kk) {
-#pragma unroll
-          for (int e = 0; e < 3; ++e)
-#pragma unroll
-            for (int j = 0; j < 12; ++j) Sr[e][j] = Sp[12 * (3 * q + e) + j];
-        }
-        sync_all<NW>();
+        sync_all();
       }
       // a non-positive pivot anywhere fails the whole instance (uniform result)
       if (!ok) atomicOr(&sh.flag[2], 1);
-      sync_all<NW>();
+      sync_all();
       const bool good = sh.flag[2] == 0;
-      sync_all<NW>();
+      sync_all();
       return good;
-    };
-
-    // ---- KKT solve: (bf, bX) own columns -> (sf, sX) own columns ----------
-    auto kkt_solve = [&](const double (&bf)[3], const double (&bX)[3], double (&sf)[3],
-                         double (&sX)[3]) __attribute__((always_inline)) {
-      double ball[12], u[3];
-      quad_gather12(bf, ball);
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        double s = 0.0;
-#pragma unroll
-        for (int j = 0; j < 12; ++j) s += Fr[e][j] * ball[j];
-        u[e] = s;
-      }
-      double bu6[6];
-      Bf6(u, bu6);  // beta = rho (B u)_{6..11}
-      if (q == 0) {
-#pragma unroll
-        for (int j = 0; j < 6; ++j) sh.u.it.be[k][j] = rho_dyn(k, 6 + j) * bu6[j];
-      }
-      // bt_X without the next stage's beta term (the recurrence adds it)
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        const int i = 3 * q + e;
-        double bt = bX[e];
-        if (q >= 2) {
-          const double bown = rho_dyn(k, i) * (q == 2 ? bu6[e] : bu6[3 + e]);
-          bt -= A.Xd(k, i) * bown;
-        }
-        sh.u.it.ws[k][i] = bt;
-      }
-      sync_all<NW>();
-      STAMP(4);
-      // forward recurrence y_k = bt_k - Hd_{k+1} beta_{k+1} - G_k y_{k-1} (wave 0, lane (r, cb))
-      if (wv == 0) {
-        const int r = lane >> 2, cb = lane & 3;
-        const bool act = lane < 48;
-        double p0 = 0.0, p1 = 0.0, p2 = 0.0;
-        for (int kk = 0; kk < N; ++kk) {
-          double g0 = 0.0, g1 = 0.0, g2 = 0.0, bt = 0.0;
-          if (act) {
-            const double* G = sh.Gm[kk] + 12 * r + 3 * cb;
-            g0 = G[0]; g1 = G[1]; g2 = G[2];
-            bt = sh.u.it.ws[kk][r];
-            if (r >= 6 && kk < N - 1) bt -= A.Hd(kk + 1, r) * sh.u.it.be[kk + 1][r - 6];
-          }
-          double acc = g0 * p0 + g1 * p1 + g2 * p2;
-          acc = quad_sum(acc);
-          const double yr = bt - acc;
-          if (act && cb == 0) sh.u.it.ws[kk][r] = yr;
-          p0 = __shfl(yr, 4 * (3 * cb + 0));
-          p1 = __shfl(yr, 4 * (3 * cb + 1));
-          p2 = __shfl(yr, 4 * (3 * cb + 2));
-        }
-      }
-      sync_all<NW>();
-      STAMP(5);
-      // w_k = S_k^{-1} y_k
-      {
-        double yall[12];
-#pragma unroll
-        for (int j = 0; j < 12; ++j) yall[j] = sh.u.it.ws[k][j];
-#pragma unroll
-        for (int e = 0; e < 3; ++e) {
-          double s = 0.0;
-#pragma unroll
-          for (int j = 0; j < 12; ++j) s += Sr[e][j] * yall[j];
-          sh.u.it.xs[k][3 * q + e] = s;
-        }
-      }
-      sync_all<NW>();
-      STAMP(6);
-      // backward recurrence X_k = w_k - G_{k+1}' X_{k+1}
-      if (wv == 0) {
-        const int r = lane >> 2, cb = lane & 3;
-        const bool act = lane < 48;
-        double p0 = 0.0, p1 = 0.0, p2 = 0.0;
-        for (int kk = N - 1; kk >= 0; --kk) {
-          double g0 = 0.0, g1 = 0.0, g2 = 0.0, w = 0.0;
-          if (act) {
-            w = sh.u.it.xs[kk][r];
-            if (kk < N - 1) {
-              const double* G = sh.Gm[kk + 1] + r;
-              g0 = G[12 * (3 * cb + 0)]; g1 = G[12 * (3 * cb + 1)]; g2 = G[12 * (3 * cb + 2)];
-            }
-          }
-          double acc = g0 * p0 + g1 * p1 + g2 * p2;
-          acc = quad_sum(acc);
-          const double xr = w - acc;
-          if (act && cb == 0) sh.u.it.xs[kk][r] = xr;
-          p0 = __shfl(xr, 4 * (3 * cb + 0));
-          p1 = __shfl(xr, 4 * (3 * cb + 1));
-          p2 = __shfl(xr, 4 * (3 * cb + 2));
-        }
-      }
-      sync_all<NW>();
-      STAMP(7);
-      // forces: f_k = F_k (b_f - W_k gamma_k)
-      double gam[6];
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const int i = 6 + j;
-        double g = A.Xd(k, i) * sh.u.it.xs[k][i];
-        if (k >= 1) g += A.Hd(k, i) * sh.u.it.xs[k - 1][i];
-        gam[j] = rho_dyn(k, i) * g;
-      }
-      double rf[3], rall[12];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const int fo = FO<N>(k, q, c);
-        double wg = sh.Ab[fo] * gam[c];
-        wg += sh.Ab[fo + 1] * gam[3];
-        wg += sh.Ab[fo + 2] * gam[4];
-        wg += sh.Ab[fo + 3] * gam[5];
-        rf[c] = bf[c] - wg;
-      }
-      quad_gather12(rf, rall);
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        double s = 0.0;
-#pragma unroll
-        for (int j = 0; j < 12; ++j) s += Fr[e][j] * rall[j];
-        sf[e] = s;
-        sX[e] = sh.u.it.xs[k][3 * q + e];
-      }
     };
 
     // ---- residuals (OSQP update_info), uniform results ---------------------
     double pri_res = 0.0, dua_res = 0.0, eps_pri = 0.0, eps_dua = 0.0, s_pri = 0.0, s_dua = 0.0;
     auto update_info = [&]() __attribute__((always_inline)) {
-      sync_all<NW>();
-#pragma unroll
-      for (int e = 0; e < 3; ++e) { sh.u.it.xs[k][3 * q + e] = x[3 + e]; sh.u.it.bd[k][3 * q + e] = y[e]; }
-      sync_all<NW>();
+      sync_all();
+      if (cl) { sh.u.it.xs[k + 1][ph] = xX; sh.u.it.xw[k][ph] = y[0]; }
+      sync_all();
       double qv[12];
-#pragma unroll
-      for (int e = 0; e < 12; ++e) qv[e] = 0.0;
-      {
-        const double xf[3] = {x[0], x[1], x[2]}, xX[3] = {x[3], x[4], x[5]};
-        double ax[11];
+      {  // primal side: A x - z on the own rows
+        double ax[3], q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         row_A(xf, xX, ax);
 #pragma unroll
-        for (int j = 0; j < 11; ++j) {
+        for (int j = 0; j < 3; ++j) {
           const double ei = 1.0 / E[j], d = ax[j] - z[j];
-          qv[0] = fmax(qv[0], fabs(ei * d));
-          qv[1] = fmax(qv[1], fabs(ei * ax[j]));
-          qv[2] = fmax(qv[2], fabs(ei * z[j]));
-          qv[3] = fmax(qv[3], fabs(d));
-          qv[4] = fmax(qv[4], fabs(ax[j]));
-          qv[5] = fmax(qv[5], fabs(z[j]));
+          q6[0] = fmax(q6[0], fabs(ei * d));
+          q6[1] = fmax(q6[1], fabs(ei * ax[j]));
+          q6[2] = fmax(q6[2], fabs(ei * z[j]));
+          q6[3] = fmax(q6[3], fabs(d));
+          q6[4] = fmax(q6[4], fabs(ax[j]));
+          q6[5] = fmax(q6[5], fabs(z[j]));
+        }
+#pragma unroll
+        for (int e = 0; e < 6; ++e) {
+          const double v = wave_max(q6[e]);
+          if ((t & 63) == 0) sh.red[12 * wv + e] = v;
         }
       }
-      {
-        double aty[6];
-        col_At(y, aty);
+      {  // dual side: P x + A' y on the own columns
+        double atf, atX, q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        col_At(y, atf, atX);
+        const double pxf = Pbf() * xf, pxX = PbX() * xX;
+        const double dif = 1.0 / Df, diX = 1.0 / DX;
+        const double df_ = pxf + atf, dX_ = pxX + atX;
+        if (cl) {
+          q6[0] = fmax(fabs(dif * df_), fabs(diX * dX_));
+          q6[1] = fmax(fabs(dif * pxf), fabs(diX * pxX));
+          q6[2] = fmax(fabs(dif * atf), fabs(diX * atX));
+          q6[3] = fmax(fabs(df_), fabs(dX_));
+          q6[4] = fmax(fabs(pxf), fabs(pxX));
+          q6[5] = fmax(fabs(atf), fabs(atX));
+        }
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
-          const double px = Pbar(j) * x[j], di = 1.0 / D[j], d = px + 0.0 + aty[j];
-          qv[6] = fmax(qv[6], fabs(di * d));
-          qv[7] = fmax(qv[7], fabs(di * px));
-          qv[8] = fmax(qv[8], fabs(di * aty[j]));
-          qv[9] = fmax(qv[9], fabs(d));
-          qv[10] = fmax(qv[10], fabs(px));
-          qv[11] = fmax(qv[11], fabs(aty[j]));
+        for (int e = 0; e < 6; ++e) {
+          const double v = wave_max(q6[e]);
+          if ((t & 63) == 0) sh.red[12 * wv + 6 + e] = v;
         }
       }
+      sync_all();
 #pragma unroll
-      for (int e = 0; e < 12; ++e) qv[e] = wave_max(qv[e]);
-      if constexpr (NW > 1) {
-        sync_all<NW>();
-        double* red = &sh.u.it.ws[0][0];
-        if (lane == 0) {
+      for (int e = 0; e < 12; ++e) {
+        double v = 0.0;
 #pragma unroll
-          for (int e = 0; e < 12; ++e) red[16 * wv + e] = qv[e];
-        }
-        sync_all<NW>();
-#pragma unroll
-        for (int e = 0; e < 12; ++e) {
-          double v = 0.0;
-#pragma unroll
-          for (int w = 0; w < NW; ++w) v = fmax(v, red[16 * w + e]);
-          qv[e] = v;
-        }
+        for (int w = 0; w < NW; ++w) v = fmax(v, sh.red[12 * w + e]);
+        qv[e] = v;
       }
       const double cinv = 1.0 / cscale;
       pri_res = qv[0];
@@ -923,178 +833,148 @@ __global__ __launch_bounds__(64 * (N / 16), 1) void engine_kernel(mpcq_params p,
       eps_dua = p.eps_abs + p.eps_rel * cinv * fmax(qv[7], qv[8]);
       s_pri = qv[3] / (fmax(qv[4], qv[5]) + kDivTol);
       s_dua = qv[9] / (fmax(qv[10], qv[11]) + kDivTol);
-      sync_all<NW>();
+      sync_all();
     };
-    auto converged = [&](double f) __attribute__((always_inline)) {
-      return pri_res < f * eps_pri && dua_res < f * eps_dua;
+    auto converged = [&](double fac) __attribute__((always_inline)) {
+      return pri_res < fac * eps_pri && dua_res < fac * eps_dua;
     };
 
     if (status == 0) {
       STAMP(0);
       // ------------------------------------------------------------ Ruiz scaling
       {
-        double Pb[6];
-#pragma unroll
-        for (int j = 0; j < 6; ++j) Pb[j] = P0(j);
+        double Pf = P0f, PX = P0X;
+        double* Ex = gh0;  // row factors of this pass: Ex[48 k + 3 s + slot]
+        // friction row t of foot fp: owner lane / slot
+        auto fr_E = [&](int kk, int fp, int t_) __attribute__((always_inline)) {
+          return t_ < 3 ? Ex[48 * kk + 3 * (4 * fp + t_) + 2] : Ex[48 * kk + 3 * (4 * fp + 3) + (t_ - 3)];
+        };
+        auto dyn_E = [&](int kk, int i) __attribute__((always_inline)) { return Ex[48 * kk + 3 * LN(i)]; };
+        auto fr_norm = [&](int t_) __attribute__((always_inline)) {
+          double v = fabs(Ab[FO<N>(k, f, 2) + 5 + t_]);
+          if (t_ < 4) v = fmax(v, fabs(Ab[FO<N>(k, f, t_ >> 1) + 5 + (t_ & 1)]));
+          return v;
+        };
         for (int it = 0; it < p.scaling; ++it) {
-          double dtv[6], etv[11];
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {  // column norms of [P; A]
-            const int fo = FO<N>(k, q, c);
-            const int cnt = c < 2 ? 7 : 10;
-            double v = fabs(Pb[c]);
-            for (int e = 0; e < cnt; ++e) v = fmax(v, fabs(sh.Ab[fo + e]));
-            dtv[c] = v;
+          double dtf = fabs(Pf);
+          {
+            const int cnt = cc < 2 ? 7 : 10;
+            for (int e = 0; e < cnt; ++e) dtf = fmax(dtf, fabs(Ab[fo + e]));
           }
-#pragma unroll
-          for (int e = 0; e < 3; ++e) {
-            const int i = 3 * q + e, xo = XO<N>(k, i);
-            const int cnt = (k < N - 1) ? (i < 6 ? 2 : 3) : 1;
-            double v = fabs(Pb[3 + e]);
-            for (int h = 0; h < cnt; ++h) v = fmax(v, fabs(sh.Ab[xo + h]));
-            dtv[3 + e] = v;
+          double dtx = fabs(PX);
+          {
+            const int cnt = (k < N - 1) ? (ph < 6 ? 2 : 3) : 1;
+            for (int h = 0; h < cnt; ++h) dtx = fmax(dtx, fabs(Ab[xo + h]));
           }
-#pragma unroll
-          for (int e = 0; e < 3; ++e) {  // row norms of A
-            const int i = 3 * q + e;
-            double v = fabs(A.Xd(k, i));
+          double et[3];
+          {
+            double v = fabs(Xd(k, ph));
             if (k >= 1) {
-              v = fmax(v, fabs(A.Hd(k, i)));
-              if (i < 6) v = fmax(v, fabs(A.H6(k, i)));
+              v = fmax(v, fabs(Hd(k, ph)));
+              if (ph < 6) v = fmax(v, fabs(H6(k, ph)));
             }
-            if (q == 2) {
+            if (ph >= 6) {
 #pragma unroll
-              for (int f = 0; f < 4; ++f) v = fmax(v, fabs(sh.Ab[FO<N>(k, f, e)]));
-            } else if (q == 3) {
-#pragma unroll
-              for (int f = 0; f < 4; ++f)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) v = fmax(v, fabs(sh.Ab[FO<N>(k, f, c) + 1 + e]));
+              for (int psi = 0; psi < 12; ++psi) v = fmax(v, fabs(Bc(k, ph, psi / 3, psi % 3)));
             }
-            etv[e] = v;
+            et[0] = cl ? v : fr_norm(3);
+            et[1] = cl ? fabs(Ab[fo + 4]) : fr_norm(4);
+            et[2] = cl ? fr_norm(c) : 0.0;
           }
+          dtf = dtf < kMinScaling ? 1.0 : (dtf > kMaxScaling ? kMaxScaling : dtf);
+          dtx = dtx < kMinScaling ? 1.0 : (dtx > kMaxScaling ? kMaxScaling : dtx);
+          dtf = 1.0 / sqrt(dtf);
+          dtx = 1.0 / sqrt(dtx);
+          Df *= dtf;
+          DX *= dtx;
+          Pf = dtf * Pf * dtf;
+          PX = dtx * PX * dtx;
 #pragma unroll
-          for (int c = 0; c < 3; ++c) etv[3 + c] = fabs(A.Sw(k, q, c));
-          {
-            const int b0 = FO<N>(k, q, 0), b1 = FO<N>(k, q, 1), b2 = FO<N>(k, q, 2);
-            etv[6] = fmax(fabs(sh.Ab[b0 + 5]), fabs(sh.Ab[b2 + 5]));
-            etv[7] = fmax(fabs(sh.Ab[b0 + 6]), fabs(sh.Ab[b2 + 6]));
-            etv[8] = fmax(fabs(sh.Ab[b1 + 5]), fabs(sh.Ab[b2 + 7]));
-            etv[9] = fmax(fabs(sh.Ab[b1 + 6]), fabs(sh.Ab[b2 + 8]));
-            etv[10] = fabs(sh.Ab[b2 + 9]);
-          }
-#pragma unroll
-          for (int j = 0; j < 6; ++j) {
-            double v = dtv[j];
+          for (int j = 0; j < 3; ++j) {
+            double v = et[j];
             v = v < kMinScaling ? 1.0 : (v > kMaxScaling ? kMaxScaling : v);
-            dtv[j] = 1.0 / sqrt(v);
-            D[j] *= dtv[j];
-            Pb[j] = dtv[j] * Pb[j] * dtv[j];
+            et[j] = 1.0 / sqrt(v);
+            E[j] *= et[j];
           }
 #pragma unroll
-          for (int j = 0; j < 11; ++j) {
-            double v = etv[j];
-            v = v < kMinScaling ? 1.0 : (v > kMaxScaling ? kMaxScaling : v);
-            etv[j] = 1.0 / sqrt(v);
-            E[j] *= etv[j];
-          }
-          // exchange the dyn-row factors; scale own columns' entries (E_r A D_c)
+          for (int j = 0; j < 3; ++j) Ex[48 * k + 3 * s + j] = et[j];
+          sync_all();
+          if (cl) {  // own columns: E_row A D_col
+            const double dA = dyn_E(k, 6 + cc);
+            sh.Ab[fo] = dA * sh.Ab[fo] * dtf;
 #pragma unroll
-          for (int e = 0; e < 3; ++e) sh.u.it.bd[k][3 * q + e] = etv[e];
-          sync_all<NW>();
-          {
-            const double* ek = sh.u.it.bd[k];
+            for (int j = 0; j < 3; ++j) sh.Ab[fo + 1 + j] = dyn_E(k, 9 + j) * sh.Ab[fo + 1 + j] * dtf;
+            sh.Ab[fo + 4] = et[1] * sh.Ab[fo + 4] * dtf;
+            if (cc < 2) {
+              sh.Ab[fo + 5] = fr_E(k, f, 2 * cc) * sh.Ab[fo + 5] * dtf;
+              sh.Ab[fo + 6] = fr_E(k, f, 2 * cc + 1) * sh.Ab[fo + 6] * dtf;
+            } else {
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-              const int fo = FO<N>(k, q, c);
-              const double dt = dtv[c];
-              sh.Ab[fo] = ek[6 + c] * sh.Ab[fo] * dt;
-              sh.Ab[fo + 1] = ek[9] * sh.Ab[fo + 1] * dt;
-              sh.Ab[fo + 2] = ek[10] * sh.Ab[fo + 2] * dt;
-              sh.Ab[fo + 3] = ek[11] * sh.Ab[fo + 3] * dt;
-              sh.Ab[fo + 4] = etv[3 + c] * sh.Ab[fo + 4] * dt;
-              if (c == 0) { sh.Ab[fo + 5] = etv[6] * sh.Ab[fo + 5] * dt; sh.Ab[fo + 6] = etv[7] * sh.Ab[fo + 6] * dt; }
-              else if (c == 1) { sh.Ab[fo + 5] = etv[8] * sh.Ab[fo + 5] * dt; sh.Ab[fo + 6] = etv[9] * sh.Ab[fo + 6] * dt; }
-              else {
-#pragma unroll
-                for (int tt = 0; tt < 5; ++tt) sh.Ab[fo + 5 + tt] = etv[6 + tt] * sh.Ab[fo + 5 + tt] * dt;
-              }
+              for (int t_ = 0; t_ < 5; ++t_) sh.Ab[fo + 5 + t_] = fr_E(k, f, t_) * sh.Ab[fo + 5 + t_] * dtf;
             }
-#pragma unroll
-            for (int e = 0; e < 3; ++e) {
-              const int i = 3 * q + e, xo = XO<N>(k, i);
-              const double dt = dtv[3 + e];
-              sh.Ab[xo] = etv[e] * sh.Ab[xo] * dt;
-              if (k < N - 1) {
-                const double* en = sh.u.it.bd[k + 1];
-                if (i >= 6) {
-                  sh.Ab[xo + 1] = en[i - 6] * sh.Ab[xo + 1] * dt;
-                  sh.Ab[xo + 2] = en[i] * sh.Ab[xo + 2] * dt;
-                } else {
-                  sh.Ab[xo + 1] = en[i] * sh.Ab[xo + 1] * dt;
-                }
+            sh.Ab[xo] = et[0] * sh.Ab[xo] * dtx;
+            if (k < N - 1) {
+              if (ph >= 6) {
+                sh.Ab[xo + 1] = dyn_E(k + 1, ph - 6) * sh.Ab[xo + 1] * dtx;
+                sh.Ab[xo + 2] = dyn_E(k + 1, ph) * sh.Ab[xo + 2] * dtx;
+              } else {
+                sh.Ab[xo + 1] = dyn_E(k + 1, ph) * sh.Ab[xo + 1] * dtx;
               }
             }
           }
           // cost scaling: c = 1 / max(mean |P|, 1)  (q = 0)
-          double ps = 0.0;
-#pragma unroll
-          for (int j = 0; j < 6; ++j) ps += fabs(Pb[j]);
+          double ps = cl ? fabs(Pf) + fabs(PX) : 0.0;
           ps = wave_sum(ps);
-          if constexpr (NW > 1) {
-            double* red = sh.u.it.ws[0];
-            sync_all<NW>();
-            if (lane == 0) red[wv] = ps;
-            sync_all<NW>();
-            ps = 0.0;
+          if ((t & 63) == 0) sh.red[wv] = ps;
+          sync_all();
+          ps = 0.0;
 #pragma unroll
-            for (int w = 0; w < NW; ++w) ps += red[w];
-          }
+          for (int w = 0; w < NW; ++w) ps += sh.red[w];
           const double mean = ps / n;
           double ctmp = mean > 1.0 ? mean : 1.0;
           ctmp = ctmp < kMinScaling ? 1.0 : (ctmp > kMaxScaling ? kMaxScaling : ctmp);
           ctmp = 1.0 / ctmp;
-#pragma unroll
-          for (int j = 0; j < 6; ++j) Pb[j] *= ctmp;
-          cscale *= ctmp;
-          sync_all<NW>();
+          Pf *= ctmp;
+          PX *= ctmp;
+          cscale = uni(cscale * ctmp);
+          sync_all();
         }
       }
       // scaled bounds, constraint classes (osqp set_rho_vec)
       if constexpr (FUSED) {
-#pragma unroll
-        for (int e = 0; e < 3; ++e) bnd[e] *= E[e];
+        bnd *= E[0];
       } else {
 #pragma unroll
-        for (int j = 0; j < 11; ++j) { lo_g[j] *= E[j]; hi_g[j] *= E[j]; }
+        for (int j = 0; j < 3; ++j) { lo_g[j] *= E[j]; hi_g[j] *= E[j]; }
       }
 #pragma unroll
-      for (int j = 0; j < 11; ++j) {
+      for (int j = 0; j < 3; ++j) {
         const double lj = lo_of(j), hj = hi_of(j);
-        unsigned int c;
-        if (lj < -kInf * kMinScaling && hj > kInf * kMinScaling) c = RC_LOOSE;
-        else if (hj - lj < kRhoTol) c = RC_EQ;
-        else c = RC_INEQ;
-        if (j < 10) cpack0 |= c << (3 * j);
-        else cpack1 |= c << (3 * (j - 10));
-        sh.rc[44 * k + row_i(j)] = (unsigned char)c;
+        unsigned cj;
+        if (lj < -kInf * kMinScaling && hj > kInf * kMinScaling) cj = RC_LOOSE;
+        else if (hj - lj < kRhoTol) cj = RC_EQ;
+        else cj = RC_INEQ;
+        cls |= cj << (2 * j);
       }
+      set_rho();
       // warm start (osqp_warm_start: x = D^-1 x0, z = A x; y = c E^-1 y0)
       if (a.warm_x) {
-#pragma unroll
-        for (int j = 0; j < 6; ++j) x[j] = a.warm_x[b * n + nat_col(j)] / D[j];
-#pragma unroll
-        for (int e = 0; e < 3; ++e) sh.u.it.xs[k][3 * q + e] = x[3 + e];
-        sync_all<NW>();
-        const double xf[3] = {x[0], x[1], x[2]}, xX[3] = {x[3], x[4], x[5]};
+        xf = a.warm_x[b * n + colF] / Df;
+        xX = a.warm_x[b * n + colX] / DX;
+        if (cl) sh.u.it.xs[k + 1][ph] = xX;
+        sync_all();
         row_A(xf, xX, z);
-        sync_all<NW>();
+        if (!cl) z[2] = 0.0;
+        sync_all();
       }
       if (a.warm_y) {
 #pragma unroll
-        for (int j = 0; j < 11; ++j) y[j] = cscale * a.warm_y[b * m + nat_row(j)] / E[j];
+        for (int j = 0; j < 3; ++j) {
+          const int r = nat_row(j);
+          y[j] = r >= 0 ? cscale * a.warm_y[b * m + r] / E[j] : 0.0;
+        }
       }
-      sync_all<NW>();
+      sync_all();
       STAMP(1);
 
       // ------------------------------------------------------------ ADMM
@@ -1107,48 +987,180 @@ __global__ __launch_bounds__(64 * (N / 16), 1) void engine_kernel(mpcq_params p,
         STAMP(2);
         bool refactor = false;
         for (; iter <= p.max_iter; ++iter) {
-          // w = rho z - y (own rows); dyn rows exchanged through LDS
-          double w[11];
+          launder();
+          // P1: w = rho z - y (own rows); dynamics w to LDS for the previous stage's states
+          double w[3];
 #pragma unroll
-          for (int j = 0; j < 11; ++j) w[j] = rho(cls(j)) * z[j] - y[j];
-#pragma unroll
-          for (int e = 0; e < 3; ++e) sh.u.it.bd[k][3 * q + e] = w[e];
-          sync_all<NW>();
+          for (int j = 0; j < 3; ++j) w[j] = rho_of(j) * z[j] - y[j];
+          if (cl) sh.u.it.xw[k][ph] = w[0];
+          sync_all();
           STAMP(3);
-          double bf[3], bX[3];
+          // P2: b = sigma x + A' w;  P3: u = F b_f, beta = R B u
+          double bf, bX;
+          col_At(w, bf, bX);
+          bf += p.sigma * xf;  // - q, q = 0
+          bX += p.sigma * xX;
+          double beta;
           {
-            double bv[6];
-            col_At(w, bv);
+            double ball[12], uall[12];
+            gather12(bf, ball);
+            double uf = 0.0;
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-              bf[j] = bv[j] + p.sigma * x[j];  // - q, q = 0
-              bX[j] = bv[3 + j] + p.sigma * x[3 + j];
+            for (int j = 0; j < 12; ++j) uf += Fr[j] * ball[j];
+            gather12(uf, uall);
+            double bu = 0.0;
+#pragma unroll
+            for (int psi = 0; psi < 12; ++psi) bu += Bc(k, ph, psi / 3, psi % 3) * uall[psi];
+            beta = rho_of(0) * bu;
+          }
+          if (cl && ph >= 6) sh.u.it.be[k][ph - 6] = beta;
+          sync_all();
+          STAMP(4);
+          // P4: sweep right-hand side bt = b_X - K_Xf u
+          {
+            const double ben = sh.u.it.be[k < N - 1 ? k + 1 : k][ph >= 6 ? ph - 6 : 0];
+            const double t1 = bX - Ab[xo] * beta;
+            const double t2 = t1 - Ab[xo + 2] * ben;  // Hd(k+1, ph), ph >= 6
+            const double bt = ph >= 6 ? (k < N - 1 ? t2 : t1) : bX;
+            if (cl) sh.u.it.xw[k][ph] = bt;
+          }
+          sync_all();
+          STAMP(5);
+          // P5: the two inward sweeps (wave 0, rows 0 and 1), meeting at MID
+          double xm = 0.0;
+          if (t < 32) {
+            // step j: top row kk = j (G_kk in GH[kk]); bottom row kk = N-1-j (H_kk in GH[kk+1])
+            auto kk_of = [&](int j) __attribute__((always_inline)) { return cr == 0 ? j : N - 1 - j; };
+            auto slot_of = [&](int j) __attribute__((always_inline)) {
+              return cr == 0 ? j : (N - j < N ? N - j : N - 1);
+            };
+            const int k0 = cr == 0 ? 0 : N - 1;
+            double yp = sh.u.it.xw[k0][rr_];
+            if (s < 12) sh.u.it.yv[k0][rr_] = yp;
+            double g[12], bq;
+            {
+              lds_cd* M = GHr + 144 * slot_of(1) + 12 * rr_;
+#pragma unroll
+              for (int jj = 0; jj < 12; ++jj) g[jj] = M[jj];
+              bq = sh.u.it.xw[kk_of(1)][rr_];
+            }
+#pragma unroll
+            for (int j = 1; j <= MID; ++j) {
+              launder();
+              double gc[12];
+#pragma unroll
+              for (int jj = 0; jj < 12; ++jj) gc[jj] = g[jj];
+              const double bc = bq;
+              if (j < MID) {  // prefetch the next step's matrix row and right-hand side
+                lds_cd* M = GHr + 144 * slot_of(j + 1) + 12 * rr_;
+#pragma unroll
+                for (int jj = 0; jj < 12; ++jj) g[jj] = M[jj];
+                bq = sh.u.it.xw[kk_of(j + 1)][rr_];
+              }
+              const double acc = bc - dotr12(gc, yp);
+              const int kk = kk_of(j);
+              const bool act = cr == 0 || kk >= MID;
+              yp = act ? acc : yp;
+              if (act && kk != MID && s < 12) sh.u.it.yv[kk][rr_] = acc;
+            }
+            sh.red[RMID + 16 * cr + s] = yp;
+            wave_sync();
+            const double cm = sh.red[RMID + rr_] + sh.red[RMID + 16 + rr_] - sh.u.it.xw[MID][rr_];
+            xm = dotb12(GHr + 12 * rr_, 1, cm);
+            if (cr == 0 && s < 12) sh.u.it.xs[MID + 1][rr_] = xm;
+          }
+          sync_all();
+          STAMP(6);
+          // P6: w_k = S_k^{-1} y_k in place (every stage but MID)
+          if (k != MID) {
+            double yall[12];
+#pragma unroll
+            for (int j = 0; j < 12; ++j) yall[j] = sh.u.it.yv[k][j];
+            double acc = 0.0;
+#pragma unroll
+            for (int j = 0; j < 12; ++j) acc += Sr[j] * yall[j];
+            wave_sync();
+            if (cl) sh.u.it.yv[k][ph] = acc;
+          }
+          sync_all();
+          STAMP(7);
+          // P7: the two outward sweeps
+          if (t < 32) {
+            // step j: top row kk = MID-j (G_{kk+1}' from GH[kk+1]); bottom row kk = MID+j
+            // (H_{kk-1}' from GH[kk]); matrices read by column
+            auto kk_of = [&](int j) __attribute__((always_inline)) { return cr == 0 ? MID - j : MID + j; };
+            auto kc_of = [&](int j) __attribute__((always_inline)) {
+              const int kk = kk_of(j);
+              return kk <= N - 1 ? kk : N - 1;
+            };
+            auto slot_of = [&](int j) __attribute__((always_inline)) { return cr == 0 ? MID - j + 1 : kc_of(j); };
+            double xp = xm;
+            double g[12], bq;
+            {
+              lds_cd* M = GHr + 144 * slot_of(1) + rr_;
+#pragma unroll
+              for (int jj = 0; jj < 12; ++jj) g[jj] = M[12 * jj];
+              bq = sh.u.it.yv[kc_of(1)][rr_];
+            }
+#pragma unroll
+            for (int j = 1; j <= MID; ++j) {
+              launder();
+              double gc[12];
+#pragma unroll
+              for (int jj = 0; jj < 12; ++jj) gc[jj] = g[jj];
+              const double bc = bq;
+              if (j < MID) {
+                lds_cd* M = GHr + 144 * slot_of(j + 1) + rr_;
+#pragma unroll
+                for (int jj = 0; jj < 12; ++jj) g[jj] = M[12 * jj];
+                bq = sh.u.it.yv[kc_of(j + 1)][rr_];
+              }
+              const double acc = bc - dotr12(gc, xp);
+              const int kk = kk_of(j);
+              const bool act = cr == 0 || kk <= N - 1;
+              xp = act ? acc : xp;
+              if (act && s < 12) sh.u.it.xs[kk + 1][rr_] = acc;
             }
           }
-          double sf[3], sX[3];
-          kkt_solve(bf, bX, sf, sX);
+          sync_all();
           STAMP(8);
-          // z, y update (osqp update_z / update_y), x update
+          // P8: forces f_k = F_k (b_f - W_k gamma_k)
+          double sf, sX;
           {
-            double ax[11];
-            row_A(sf, sX, ax);
+            sX = sh.u.it.xs[k + 1][ph];
+            double g = Ab[xo] * sX;
+            const double g1 = g + Hd(k, ph) * sh.u.it.xs[k][ph];
+            g = (k >= 1 ? g1 : g) * rho_of(0);  // used from the lanes of rows 6..11 only
+            const double gm6 = rbc<LN(6)>(g), gm7 = rbc<LN(7)>(g), gm8 = rbc<LN(8)>(g);
+            double wg = Ab[fo] * sel3(cc, gm6, gm7, gm8);
+            wg += Ab[fo + 1] * rbc<LN(9)>(g);
+            wg += Ab[fo + 2] * rbc<LN(10)>(g);
+            wg += Ab[fo + 3] * rbc<LN(11)>(g);
+            double rall[12];
+            gather12(bf - wg, rall);
+            double acc = 0.0;
 #pragma unroll
-            for (int j = 0; j < 11; ++j) {
-              const int cj = cls(j);
-              const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
-              const double tt = zr + rinv(cj) * y[j];
-              const double lj = lo_of(j), hj = hi_of(j);
-              const double zn = tt < lj ? lj : (tt > hj ? hj : tt);
-              y[j] = y[j] + rho(cj) * (zr - zn);
-              z[j] = zn;
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            x[j] = p.alpha * sf[j] + (1.0 - p.alpha) * x[j];
-            x[3 + j] = p.alpha * sX[j] + (1.0 - p.alpha) * x[3 + j];
+            for (int j = 0; j < 12; ++j) acc += Fr[j] * rall[j];
+            sf = acc;
           }
           STAMP(9);
+          // P9: z, y update (osqp update_z / update_y), x update
+          {
+            double ax[3];
+            row_A(sf, sX, ax);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
+              const double tt = zr + rinv_of(j) * y[j];
+              const double lj = lo_of(j), hj = hi_of(j);
+              const double zn = tt < lj ? lj : (tt > hj ? hj : tt);
+              y[j] = y[j] + rho_of(j) * (zr - zn);
+              z[j] = zn;
+            }
+            xf = p.alpha * sf + (1.0 - p.alpha) * xf;
+            xX = p.alpha * sX + (1.0 - p.alpha) * xX;
+          }
+          STAMP(10);
           const bool can_check = p.check_termination > 0 && (iter % p.check_termination == 0);
           const bool adapt = p.adaptive_rho && p.adaptive_rho_interval > 0 &&
                              (iter % p.adaptive_rho_interval == 0);
@@ -1162,20 +1174,16 @@ __global__ __launch_bounds__(64 * (N / 16), 1) void engine_kernel(mpcq_params p,
               rn = fmin(fmax(rn, kRhoMin), kRhoMax);
               if (rn > rho_s * p.adaptive_rho_tolerance || rn < rho_s / p.adaptive_rho_tolerance) {
                 rho_s = rn;
-                rho.v[1] = rho_s;
-                rho.v[2] = kRhoEq * rho_s;
-                rinv.v[1] = 1.0 / rho.v[1];
-                rinv.v[2] = 1.0 / rho.v[2];
+                set_rho();
                 refactor = true;
                 ++n_upd;
                 ++iter;
-                sync_all<NW>();
+                sync_all();
                 break;
               }
             }
           }
-          sync_all<NW>();
-          STAMP(10);
+          STAMP(11);
         }
         if (!refactor) break;
       }
@@ -1192,18 +1200,20 @@ __global__ __launch_bounds__(64 * (N / 16), 1) void engine_kernel(mpcq_params p,
     // ------------------------------------------------------------ outputs
     const bool nan_out = status == MPCQ_STATUS_NONFINITE || status == MPCQ_STATUS_FACTOR_FAILED ||
                          status == MPCQ_STATUS_BAD_GAIT;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const double xv = nan_out ? NAN : D[j] * x[j];
-      if (a.x) a.x[b * n + nat_col(j)] = xv;
-      if (a.f0 && k == 0 && j < 3) a.f0[b * 12 + 3 * q + j] = xv;
+    if (cl) {
+      const double vf = nan_out ? NAN : Df * xf, vX = nan_out ? NAN : DX * xX;
+      if (a.x) { a.x[b * n + colF] = vf; a.x[b * n + colX] = vX; }
+      if (a.f0 && k == 0) a.f0[b * 12 + ph] = vf;
     }
     if (a.y) {
 #pragma unroll
-      for (int j = 0; j < 11; ++j) a.y[b * m + nat_row(j)] = nan_out ? NAN : E[j] * y[j] / cscale;
+      for (int j = 0; j < 3; ++j) {
+        const int r = nat_row(j);
+        if (r >= 0) a.y[b * m + r] = nan_out ? NAN : E[j] * y[j] / cscale;
+      }
     }
 #ifdef MPCQ_STAMPS
-    STAMP(11);
+    STAMP(12);
     if (t == 0 && a.stamps) {
       for (int i = 0; i < 16; ++i) a.stamps[b * 16 + i] = st_acc[i];
     }
@@ -1225,7 +1235,7 @@ __global__ __launch_bounds__(64 * (N / 16), 1) void engine_kernel(mpcq_params p,
 template <int N>
 hipError_t launch_t(bool fused, bool solve, const mpcq_params& p, const LaunchArgs& a,
                     hipStream_t s) {
-  const dim3 grid((unsigned)a.batch), block(64 * (N / 16));
+  const dim3 grid((unsigned)a.batch), block(16 * N);
   if (!solve) hipLaunchKernelGGL((engine_kernel<N, true, false>), grid, block, 0, s, p, a);
   else if (fused) hipLaunchKernelGGL((engine_kernel<N, true, true>), grid, block, 0, s, p, a);
   else hipLaunchKernelGGL((engine_kernel<N, false, true>), grid, block, 0, s, p, a);

@@ -106,6 +106,14 @@ __device__ __forceinline__ void gather_seq(double v, double (&all)[12], std::int
 __device__ __forceinline__ void gather12(double v, double (&all)[12]) {
   gather_seq(v, all, std::make_integer_sequence<int, 12>{});
 }
+template <int... J>
+__device__ __forceinline__ void gatherd_seq(double v, double (&all)[12], std::integer_sequence<int, J...>) {
+  ((all[J] = rbc<J>(v)), ...);
+}
+// lanes 0..11 of the row, in lane order
+__device__ __forceinline__ void gather_direct12(double v, double (&all)[12]) {
+  gatherd_seq(v, all, std::make_integer_sequence<int, 12>{});
+}
 // sum_j M[j * stride] * v_j with v_j broadcast from lane j of the row (three chains for ILP)
 template <int... J>
 __device__ __forceinline__ double dotb_seq(lds_cd* M, int stride, double v, std::integer_sequence<int, J...>) {
@@ -125,6 +133,43 @@ __device__ __forceinline__ double dotr_seq(const double (&g)[12], double v, std:
 // sum_j g_j * v_j, v_j broadcast from lane j of the row
 __device__ __forceinline__ double dotr12(const double (&g)[12], double v) {
   return dotr_seq(g, v, std::make_integer_sequence<int, 12>{});
+}
+// sum_j a_j b_j over 12 terms in three interleaved chains (shorter dependency path)
+__device__ __forceinline__ double dot12(const double (&a)[12], const double (&b)[12]) {
+  double s0 = a[0] * b[0], s1 = a[1] * b[1], s2 = a[2] * b[2];
+#pragma unroll
+  for (int j = 3; j < 12; j += 3) {
+    s0 += a[j] * b[j];
+    s1 += a[j + 1] * b[j + 1];
+    s2 += a[j + 2] * b[j + 2];
+  }
+  return (s0 + s1) + s2;
+}
+// rows 2 and 3 of the wave take lane r+6 of their own row (row_ror:10); rows 0, 1 keep v
+__device__ __forceinline__ double half_shift(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp((int)b, (int)b, 0x12A, 0xC, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), 0x12A, 0xC, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// v(lane l) + v(lane l +- 32): rows 0 + 2 and rows 1 + 3, the same sum order in both halves
+__device__ __forceinline__ double pair_sum(double v) {
+  const long long b = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  const double a0 = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
+  const double a1 = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+  return a0 + a1;
+}
+template <int... J>
+__device__ __forceinline__ double dot6_seq(const double (&g)[6], double v, std::integer_sequence<int, J...>) {
+  double a0 = 0.0, a1 = 0.0;
+  (((J % 2 == 0 ? a0 : a1) += g[J] * rbc<J>(v)), ...);
+  return a0 + a1;
+}
+// sum_{i<6} g_i * v_i, v_i broadcast from lane i of the row
+__device__ __forceinline__ double dot6(const double (&g)[6], double v) {
+  return dot6_seq(g, v, std::make_integer_sequence<int, 6>{});
 }
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
@@ -257,10 +302,14 @@ struct Smem {
   // dynamics-row rho of stage k [108,120); during scaling the row factors; in
   // the prologue xref / fsteps / the gait walk.
   double GH[N][144];
+  double Sm[N][144];        // S_k^{-1} / U_k^{-1} / M^{-1} of stage k, row-major
   union {
     struct {
-      double xw[N][12];      // dynamics-row w (A'w), then bt (sweeps' right-hand side)
-      double be[N][6];       // beta = R B u (velocity rows)
+      // sweep right-hand side of stage k's states = bo[k] + na[k] + nb[k]: bo from
+      // stage k itself, na / nb from stage k+1's dynamics rows (Hd (w - beta), H6 w)
+      double bo[N][12];
+      double na[N][12];
+      double nb[N][12];
       double yv[N][12];      // sweep outputs y / v, then w = S^{-1} y in place
       double xs[N + 1][12];  // X_k (xs[k+1] = X_{k+1}, stage k's states)
     } it;
@@ -268,7 +317,7 @@ struct Smem {
       double St[144], Sb[144], Lt[144], Lb[144];  // sweep hand-offs of the factorisation
     } fa;
   } u;
-  double red[12 * (N / 4) + 32];  // per-wave partial reductions; [12 NW, +32) sweep meeting point
+  double red[12 * N + 32];  // per-row partial reductions [12 N); [12 N, +32) sweep meeting point
   int flag[4];
 };
 
@@ -287,7 +336,7 @@ struct Prologue {
 template <int N, bool FUSED, bool SOLVE>
 __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, LaunchArgs a) {
   constexpr int NW = N / 4, T = 16 * N, n = 24 * N, m = 44 * N, nnz = 126 * N - 18, MID = N / 2;
-  constexpr int RMID = 12 * NW;  // sweep meeting point inside red[]
+  constexpr int RMID = 12 * N;  // sweep meeting point inside red[]
   __shared__ Smem<N> sh;
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
   // lane coordinates; the loops launder them (see launder()) so that the
@@ -302,12 +351,13 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
   STAMP_DECL
   lds_cd* Ab = (lds_cd*)sh.Ab;
   lds_cd* GHr = (lds_cd*)&sh.GH[0][0];
+  lds_cd* SmR = (lds_cd*)&sh.Sm[0][0];
   double* const gh0 = &sh.GH[0][0];
   int fo = FO<N>(k, f, cc), xo = XO<N>(k, ph);  // own force / state column in Ab
-  int cr = t >> 4;                  // sweep row (wave 0): 0 top-down, 1 bottom-up
+  int cr = (t >> 4) & 1;            // sweep row (wave 0): 0 top-down, 1 bottom-up
   int rr_ = s < 12 ? s : 11;        // sweep lane's state index
   auto launder = [&]() __attribute__((always_inline)) {
-    asm volatile("" : "+v"(Ab), "+v"(GHr), "+v"(k), "+v"(f), "+v"(c), "+v"(cc), "+v"(ph), "+v"(fo), "+v"(xo),
+    asm volatile("" : "+v"(Ab), "+v"(GHr), "+v"(SmR), "+v"(k), "+v"(f), "+v"(c), "+v"(cc), "+v"(ph), "+v"(fo), "+v"(xo),
                  "+v"(cr), "+v"(rr_));
   };
   (void)lane;
@@ -487,9 +537,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     // persistent per-lane state (column values of c == 3 lanes are shadows)
     double xf = 0.0, xX = 0.0, Df = 1.0, DX = 1.0;
     double z[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0}, E[3] = {1.0, 1.0, 1.0};
-    double Fr[12], Sr[12];
+    double Fr[12];  // row ph of F_k (S_k^{-1} rows live in LDS: sh.Sm)
 #pragma unroll
-    for (int j = 0; j < 12; ++j) { Fr[j] = 0.0; Sr[j] = 0.0; }
+    for (int j = 0; j < 12; ++j) Fr[j] = 0.0;
     unsigned cls = 0u;
     double cscale = 1.0;
     int it_done = 0, n_upd = 0;
@@ -544,9 +594,10 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       const double d1 = dyn + hd * xa;
       const double d2 = d1 + h6 * xb;
       dyn = k >= 1 ? (ph < 6 ? d2 : d1) : dyn;
-      double bf = 0.0;
+      double bcf[12];
 #pragma unroll
-      for (int psi = 0; psi < 12; ++psi) bf += Bc(k, ph, psi / 3, psi % 3) * fall[psi];
+      for (int psi = 0; psi < 12; ++psi) bcf[psi] = Bc(k, ph, psi / 3, psi % 3);
+      const double bf = dot12(bcf, fall);
       dyn = ph >= 6 ? dyn + bf : dyn;
       const double g0 = qbc<0>(vf), g1 = qbc<1>(vf), g2 = qbc<2>(vf);
       const double swg = Ab[fo + 4] * vf;
@@ -554,22 +605,27 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       out[1] = cl ? swg : fric_row(4, g0, g1, g2);
       out[2] = cl ? fric_row(c, g0, g1, g2) : 0.0;
     };
-    // A' w for the own columns: wo = w of own rows, xw[k+1] = next stage's dynamics w
-    auto col_At = [&](const double (&wo)[3], double& of, double& oX) __attribute__((always_inline)) {
+    // A' w for the own columns: wo = w of own rows, wbuf[k+1] = next stage's dynamics-row w
+    // force-column part of A' w (stage-local: DPP only)
+    auto colF_At = [&](const double (&wo)[3]) __attribute__((always_inline)) -> double {
       const double w6 = rbc<LN(6)>(wo[0]), w7 = rbc<LN(7)>(wo[0]), w8 = rbc<LN(8)>(wo[0]);
       const double w9 = rbc<LN(9)>(wo[0]), w10 = rbc<LN(10)>(wo[0]), w11 = rbc<LN(11)>(wo[0]);
       const double wf0 = qbc<0>(wo[2]), wf1 = qbc<1>(wo[2]), wf2 = qbc<2>(wo[2]);
       const double wf3 = qbc<3>(wo[0]), wf4 = qbc<3>(wo[1]);
-      double sF = Ab[fo] * sel3(cc, w6, w7, w8);
-      sF += Ab[fo + 1] * w9;
-      sF += Ab[fo + 2] * w10;
-      sF += Ab[fo + 3] * w11;
-      sF += Ab[fo + 4] * wo[1];
-      sF += Ab[fo + 5] * (cc == 1 ? wf2 : wf0);
-      sF += Ab[fo + 6] * (cc == 1 ? wf3 : wf1);
+      double sA = Ab[fo] * sel3(cc, w6, w7, w8);
+      double sB = Ab[fo + 1] * w9;
+      sA += Ab[fo + 2] * w10;
+      sB += Ab[fo + 3] * w11;
+      sA += Ab[fo + 4] * wo[1];
+      sB += Ab[fo + 5] * (cc == 1 ? wf2 : wf0);
+      sA += Ab[fo + 6] * (cc == 1 ? wf3 : wf1);
       const double e7 = Ab[fo + 7], e8 = Ab[fo + 8], e9 = Ab[fo + 9];  // friction rows 2..4 (cc == 2)
-      of = cc == 2 ? ((sF + e7 * wf2) + e8 * wf3) + e9 * wf4 : sF;
-      const double* wn = sh.u.it.xw[k < N - 1 ? k + 1 : k];
+      const double sC = cc == 2 ? (e7 * wf2 + e8 * wf3) + e9 * wf4 : 0.0;
+      return (sA + sB) + sC;
+    };
+    auto col_At = [&](const double (&wo)[3], const double (*wbuf)[12], double& of, double& oX) __attribute__((always_inline)) {
+      of = colF_At(wo);
+      const double* wn = wbuf[k < N - 1 ? k + 1 : k];
       const double sX = Ab[xo] * wo[0];
       const double x1 = sX + Ab[xo + 1] * wn[ph >= 6 ? ph - 6 : ph];
       const double x2 = x1 + Ab[xo + 2] * wn[ph];
@@ -753,8 +809,10 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma unroll
           for (int ci = 0; ci < 12; ++ci) Ro[ci] = Sw[12 * ph + ci];
           gj12(Ro, ph, ok);
+          if (cl) {
 #pragma unroll
-          for (int ci = 0; ci < 12; ++ci) Sr[ci] = Ro[ci];
+            for (int ci = 0; ci < 12; ++ci) sh.Sm[k][12 * ph + ci] = Ro[ci];
+          }
           wave_sync();
           if (cl) {
             double* dst = mrow ? &sh.GH[0][0] : Sw;
@@ -774,11 +832,20 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 
     // ---- residuals (OSQP update_info), uniform results ---------------------
     double pri_res = 0.0, dua_res = 0.0, eps_pri = 0.0, eps_dua = 0.0, s_pri = 0.0, s_dua = 0.0;
+    // max over a 16-lane row: quad xor 1, xor 2, then rotations by 4 and 8
+    auto row_max = [](double v) __attribute__((always_inline)) {
+      v = fmax(v, dppd<0xB1>(v));
+      v = fmax(v, dppd<0x4E>(v));
+      v = fmax(v, dppd<0x124>(v));
+      v = fmax(v, dppd<0x128>(v));
+      return v;
+    };
     auto update_info = [&]() __attribute__((always_inline)) {
       sync_all();
-      if (cl) { sh.u.it.xs[k + 1][ph] = xX; sh.u.it.xw[k][ph] = y[0]; }
+      if (cl) { sh.u.it.xs[k + 1][ph] = xX; sh.u.it.bo[k][ph] = y[0]; }
       sync_all();
-      double qv[12];
+      launder();
+      double* const rowred = sh.red + 12 * k;  // this row's 12 partial maxima
       {  // primal side: A x - z on the own rows
         double ax[3], q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         row_A(xf, xX, ax);
@@ -794,13 +861,13 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         }
 #pragma unroll
         for (int e = 0; e < 6; ++e) {
-          const double v = wave_max(q6[e]);
-          if ((t & 63) == 0) sh.red[12 * wv + e] = v;
+          const double v = row_max(q6[e]);
+          if (s == 0) rowred[e] = v;
         }
       }
       {  // dual side: P x + A' y on the own columns
         double atf, atX, q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        col_At(y, atf, atX);
+        col_At(y, sh.u.it.bo, atf, atX);
         const double pxf = Pbf() * xf, pxX = PbX() * xX;
         const double dif = 1.0 / Df, diX = 1.0 / DX;
         const double df_ = pxf + atf, dX_ = pxX + atX;
@@ -814,17 +881,20 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         }
 #pragma unroll
         for (int e = 0; e < 6; ++e) {
-          const double v = wave_max(q6[e]);
-          if ((t & 63) == 0) sh.red[12 * wv + 6 + e] = v;
+          const double v = row_max(q6[e]);
+          if (s == 0) rowred[6 + e] = v;
         }
       }
       sync_all();
-#pragma unroll
-      for (int e = 0; e < 12; ++e) {
+      // lane s of every row reduces quantity s % 12 over the N row partials, then
+      // the row shares the 12 results by row_newbcast
+      double qv[12];
+      {
+        const int e = s < 12 ? s : s - 12;
         double v = 0.0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) v = fmax(v, sh.red[12 * w + e]);
-        qv[e] = v;
+#pragma nounroll
+        for (int r = 0; r < N; ++r) v = fmax(v, sh.red[12 * r + e]);
+        gather_direct12(v, qv);
       }
       const double cinv = 1.0 / cscale;
       pri_res = qv[0];
@@ -988,141 +1058,150 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         bool refactor = false;
         for (; iter <= p.max_iter; ++iter) {
           launder();
-          // P1: w = rho z - y (own rows); dynamics w to LDS for the previous stage's states
+          // P1-P4: w = rho z - y; b_f = sigma x_f + A_f' w and u = F b_f, beta = R B u
+          // (stage-local, DPP only); then the sweep right-hand side of the own state
+          // column (bo) and this stage's dynamics-row terms of stage k-1's state
+          // columns (na, nb): the only LDS hand-off before the sweeps.
           double w[3];
 #pragma unroll
           for (int j = 0; j < 3; ++j) w[j] = rho_of(j) * z[j] - y[j];
-          if (cl) sh.u.it.xw[k][ph] = w[0];
-          sync_all();
-          STAMP(3);
-          // P2: b = sigma x + A' w;  P3: u = F b_f, beta = R B u
-          double bf, bX;
-          col_At(w, bf, bX);
-          bf += p.sigma * xf;  // - q, q = 0
-          bX += p.sigma * xX;
+          const double bf = colF_At(w) + p.sigma * xf;  // - q, q = 0
           double beta;
           {
             double ball[12], uall[12];
             gather12(bf, ball);
-            double uf = 0.0;
-#pragma unroll
-            for (int j = 0; j < 12; ++j) uf += Fr[j] * ball[j];
+            const double uf = dot12(Fr, ball);
             gather12(uf, uall);
-            double bu = 0.0;
+            double bcu[12];
 #pragma unroll
-            for (int psi = 0; psi < 12; ++psi) bu += Bc(k, ph, psi / 3, psi % 3) * uall[psi];
+            for (int psi = 0; psi < 12; ++psi) bcu[psi] = Bc(k, ph, psi / 3, psi % 3);
+            const double bu = dot12(bcu, uall);
             beta = rho_of(0) * bu;
           }
-          if (cl && ph >= 6) sh.u.it.be[k][ph - 6] = beta;
-          sync_all();
-          STAMP(4);
-          // P4: sweep right-hand side bt = b_X - K_Xf u
           {
-            const double ben = sh.u.it.be[k < N - 1 ? k + 1 : k][ph >= 6 ? ph - 6 : 0];
-            const double t1 = bX - Ab[xo] * beta;
-            const double t2 = t1 - Ab[xo + 2] * ben;  // Hd(k+1, ph), ph >= 6
-            const double bt = ph >= 6 ? (k < N - 1 ? t2 : t1) : bX;
-            if (cl) sh.u.it.xw[k][ph] = bt;
+            const double wd = ph >= 6 ? w[0] - beta : w[0];  // dynamics-row w less the force Schur term
+            const double bo = p.sigma * xX + Ab[xo] * wd;
+            const double na = Hd(k, ph) * wd;                 // on X_k[ph], stage k-1's column ph
+            const double nb = H6(k, ph) * w[0];               // on X_k[ph+6] (ph < 6)
+            if (cl) {
+              sh.u.it.bo[k][ph] = bo;
+              if (k >= 1) {
+                sh.u.it.na[k - 1][ph] = na;
+                sh.u.it.nb[k - 1][ph < 6 ? ph + 6 : ph - 6] = ph < 6 ? nb : 0.0;
+              } else {
+                sh.u.it.na[N - 1][ph] = 0.0;  // the last stage's columns have no next stage
+                sh.u.it.nb[N - 1][ph] = 0.0;
+              }
+            }
           }
           sync_all();
+          STAMP(3);
+          STAMP(4);
           STAMP(5);
-          // P5: the two inward sweeps (wave 0, rows 0 and 1), meeting at MID
-          double xm = 0.0;
-          if (t < 32) {
-            // step j: top row kk = j (G_kk in GH[kk]); bottom row kk = N-1-j (H_kk in GH[kk+1])
+          // P5-P7: the state solve on wave 0 alone (no block barrier inside).  Rows
+          // 0 / 2 run the top-down sweep (columns 0-5 / 6-11 of each step's
+          // matrix), rows 1 / 3 the bottom-up one; the two halves of every product
+          // combine by permlane32_swap.  Inward, each step also forms
+          // w_k = S_k^{-1} y_k of the stage the previous step finished (off the
+          // dependency chain, sharing its broadcasts); then the meeting stage and
+          // the outward sweeps.
+          const int half = (t >> 5) & 1, hoff = 6 * half;
+          if (t < 64) {
+            // inward step j: top kk = j (G_kk in GH[kk]); bottom kk = N-1-j (H_kk in GH[kk+1])
             auto kk_of = [&](int j) __attribute__((always_inline)) { return cr == 0 ? j : N - 1 - j; };
-            auto slot_of = [&](int j) __attribute__((always_inline)) {
-              return cr == 0 ? j : (N - j < N ? N - j : N - 1);
+            auto slot_of = [&](int j) __attribute__((always_inline)) { return cr == 0 ? j : N - j; };
+            auto act_of = [&](int j) __attribute__((always_inline)) { return cr == 0 || kk_of(j) >= MID; };
+            auto bt_of = [&](int kk) __attribute__((always_inline)) {
+              return (sh.u.it.bo[kk][rr_] + sh.u.it.na[kk][rr_]) + sh.u.it.nb[kk][rr_];
             };
-            const int k0 = cr == 0 ? 0 : N - 1;
-            double yp = sh.u.it.xw[k0][rr_];
-            if (s < 12) sh.u.it.yv[k0][rr_] = yp;
-            double g[12], bq;
+            double yp = bt_of(kk_of(0));
+            double g[6], sv[6], bq;
             {
-              lds_cd* M = GHr + 144 * slot_of(1) + 12 * rr_;
+              lds_cd* M = GHr + 144 * slot_of(1) + 12 * rr_ + hoff;
+              lds_cd* S = SmR + 144 * kk_of(0) + 12 * rr_ + hoff;
 #pragma unroll
-              for (int jj = 0; jj < 12; ++jj) g[jj] = M[jj];
-              bq = sh.u.it.xw[kk_of(1)][rr_];
+              for (int i = 0; i < 6; ++i) { g[i] = M[i]; sv[i] = S[i]; }
+              bq = bt_of(kk_of(1));
             }
 #pragma unroll
             for (int j = 1; j <= MID; ++j) {
               launder();
-              double gc[12];
+              double gc[6], sc[6];
 #pragma unroll
-              for (int jj = 0; jj < 12; ++jj) gc[jj] = g[jj];
+              for (int i = 0; i < 6; ++i) { gc[i] = g[i]; sc[i] = sv[i]; }
               const double bc = bq;
-              if (j < MID) {  // prefetch the next step's matrix row and right-hand side
-                lds_cd* M = GHr + 144 * slot_of(j + 1) + 12 * rr_;
+              if (j < MID) {  // prefetch the next step's half rows and right-hand side
+                lds_cd* M = GHr + 144 * slot_of(j + 1) + 12 * rr_ + hoff;
+                lds_cd* S = SmR + 144 * kk_of(j) + 12 * rr_ + hoff;
 #pragma unroll
-                for (int jj = 0; jj < 12; ++jj) g[jj] = M[jj];
-                bq = sh.u.it.xw[kk_of(j + 1)][rr_];
+                for (int i = 0; i < 6; ++i) { g[i] = M[i]; sv[i] = S[i]; }
+                bq = bt_of(kk_of(j + 1));
               }
-              const double acc = bc - dotr12(gc, yp);
-              const int kk = kk_of(j);
-              const bool act = cr == 0 || kk >= MID;
-              yp = act ? acc : yp;
-              if (act && kk != MID && s < 12) sh.u.it.yv[kk][rr_] = acc;
+              double yb[6];
+              {
+                const double ys = half_shift(yp);
+                yb[0] = rbc<0>(ys); yb[1] = rbc<1>(ys); yb[2] = rbc<2>(ys);
+                yb[3] = rbc<3>(ys); yb[4] = rbc<4>(ys); yb[5] = rbc<5>(ys);
+              }
+              const double acc = bc - pair_sum(((gc[0] * yb[0] + gc[2] * yb[2]) + gc[4] * yb[4]) +
+                                               ((gc[1] * yb[1] + gc[3] * yb[3]) + gc[5] * yb[5]));
+              // off the chain: w of the stage finished by the previous step
+              const double wv = pair_sum(((sc[0] * yb[0] + sc[2] * yb[2]) + sc[4] * yb[4]) +
+                                         ((sc[1] * yb[1] + sc[3] * yb[3]) + sc[5] * yb[5]));
+              const int kp = kk_of(j - 1);
+              if ((j == 1 || act_of(j - 1)) && kp != MID && half == 0 && s < 12) sh.u.it.yv[kp][rr_] = wv;
+              yp = act_of(j) ? acc : yp;
             }
-            sh.red[RMID + 16 * cr + s] = yp;
+            // meeting stage: x_m = M^{-1} (y_m + v_m - b_m)
+            if (half == 0) sh.red[RMID + 16 * cr + s] = yp;
             wave_sync();
-            const double cm = sh.red[RMID + rr_] + sh.red[RMID + 16 + rr_] - sh.u.it.xw[MID][rr_];
-            xm = dotb12(GHr + 12 * rr_, 1, cm);
-            if (cr == 0 && s < 12) sh.u.it.xs[MID + 1][rr_] = xm;
-          }
-          sync_all();
-          STAMP(6);
-          // P6: w_k = S_k^{-1} y_k in place (every stage but MID)
-          if (k != MID) {
-            double yall[12];
+            double xp;
+            {
+              const double cm = sh.red[RMID + rr_] + sh.red[RMID + 16 + rr_] - bt_of(MID);
+              double gm[6];
 #pragma unroll
-            for (int j = 0; j < 12; ++j) yall[j] = sh.u.it.yv[k][j];
-            double acc = 0.0;
+              for (int i = 0; i < 6; ++i) gm[i] = GHr[12 * rr_ + hoff + i];
+              xp = pair_sum(dot6(gm, half_shift(cm)));
+              if (cr == 0 && half == 0 && s < 12) sh.u.it.xs[MID + 1][rr_] = xp;
+            }
+            STAMP(6);
+            // outward step j: top kk = MID-j (G_{kk+1}' from GH[kk+1]); bottom kk = MID+j
+            // (H_{kk-1}' from GH[kk]); matrices read by column
+            auto ok_of = [&](int j) __attribute__((always_inline)) { return cr == 0 ? MID - j : MID + j; };
+            auto okc_of = [&](int j) __attribute__((always_inline)) {
+              const int kk = ok_of(j);
+              return kk <= N - 1 ? kk : N - 1;
+            };
+            auto oslot_of = [&](int j) __attribute__((always_inline)) { return cr == 0 ? MID - j + 1 : okc_of(j); };
+            {
+              lds_cd* M = GHr + 144 * oslot_of(1) + rr_ + 12 * hoff;
 #pragma unroll
-            for (int j = 0; j < 12; ++j) acc += Sr[j] * yall[j];
-            wave_sync();
-            if (cl) sh.u.it.yv[k][ph] = acc;
+              for (int i = 0; i < 6; ++i) g[i] = M[12 * i];
+            }
+            wave_sync();  // the w written by the inward rows
+            bq = sh.u.it.yv[okc_of(1)][rr_];
+#pragma unroll
+            for (int j = 1; j <= MID; ++j) {
+              launder();
+              double gc[6];
+#pragma unroll
+              for (int i = 0; i < 6; ++i) gc[i] = g[i];
+              const double bc = bq;
+              if (j < MID) {
+                lds_cd* M = GHr + 144 * oslot_of(j + 1) + rr_ + 12 * hoff;
+#pragma unroll
+                for (int i = 0; i < 6; ++i) g[i] = M[12 * i];
+                bq = sh.u.it.yv[okc_of(j + 1)][rr_];
+              }
+              const double acc = bc - pair_sum(dot6(gc, half_shift(xp)));
+              const int kk = ok_of(j);
+              const bool act = cr == 0 || kk <= N - 1;
+              xp = act ? acc : xp;
+              if (act && half == 0 && s < 12) sh.u.it.xs[kk + 1][rr_] = acc;
+            }
           }
           sync_all();
           STAMP(7);
-          // P7: the two outward sweeps
-          if (t < 32) {
-            // step j: top row kk = MID-j (G_{kk+1}' from GH[kk+1]); bottom row kk = MID+j
-            // (H_{kk-1}' from GH[kk]); matrices read by column
-            auto kk_of = [&](int j) __attribute__((always_inline)) { return cr == 0 ? MID - j : MID + j; };
-            auto kc_of = [&](int j) __attribute__((always_inline)) {
-              const int kk = kk_of(j);
-              return kk <= N - 1 ? kk : N - 1;
-            };
-            auto slot_of = [&](int j) __attribute__((always_inline)) { return cr == 0 ? MID - j + 1 : kc_of(j); };
-            double xp = xm;
-            double g[12], bq;
-            {
-              lds_cd* M = GHr + 144 * slot_of(1) + rr_;
-#pragma unroll
-              for (int jj = 0; jj < 12; ++jj) g[jj] = M[12 * jj];
-              bq = sh.u.it.yv[kc_of(1)][rr_];
-            }
-#pragma unroll
-            for (int j = 1; j <= MID; ++j) {
-              launder();
-              double gc[12];
-#pragma unroll
-              for (int jj = 0; jj < 12; ++jj) gc[jj] = g[jj];
-              const double bc = bq;
-              if (j < MID) {
-                lds_cd* M = GHr + 144 * slot_of(j + 1) + rr_;
-#pragma unroll
-                for (int jj = 0; jj < 12; ++jj) g[jj] = M[12 * jj];
-                bq = sh.u.it.yv[kc_of(j + 1)][rr_];
-              }
-              const double acc = bc - dotr12(gc, xp);
-              const int kk = kk_of(j);
-              const bool act = cr == 0 || kk <= N - 1;
-              xp = act ? acc : xp;
-              if (act && s < 12) sh.u.it.xs[kk + 1][rr_] = acc;
-            }
-          }
-          sync_all();
           STAMP(8);
           // P8: forces f_k = F_k (b_f - W_k gamma_k)
           double sf, sX;
@@ -1138,10 +1217,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             wg += Ab[fo + 3] * rbc<LN(11)>(g);
             double rall[12];
             gather12(bf - wg, rall);
-            double acc = 0.0;
-#pragma unroll
-            for (int j = 0; j < 12; ++j) acc += Fr[j] * rall[j];
-            sf = acc;
+            sf = dot12(Fr, rall);
           }
           STAMP(9);
           // P9: z, y update (osqp update_z / update_y), x update

@@ -13,8 +13,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "mpc-tsid_amd"))
 os.environ.setdefault("MPCQ_LIB_VARIANT", "stamps")
 
-NAMES = ["prologue", "scaling", "factor", "iter:w", "iter:b,u,beta", "iter:bt", "iter:inward sweeps",
-         "iter:S^-1 y", "iter:outward sweeps", "iter:forces", "iter:z/y/x update", "iter:check+adapt", "epilogue"]
+NAMES = ["prologue", "scaling", "factor", "iter:w,b,u,beta,bt", "-", "-", "iter:inward sweeps+S^-1 y",
+         "iter:outward sweeps", "-", "iter:forces", "iter:z/y/x update", "iter:check+adapt", "epilogue"]
 
 
 def main():

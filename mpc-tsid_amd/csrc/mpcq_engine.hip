@@ -303,6 +303,8 @@ struct Smem {
   // the prologue xref / fsteps / the gait walk.
   double GH[N][144];
   double Sm[N][144];        // S_k^{-1} / U_k^{-1} / M^{-1} of stage k, row-major
+  double FWs[N][72];        // F_k W_k (12x6, row psi at [6 psi]); W_k = B_k' R on rows 6..11
+  double QL[N][36];         // B_k F_k W_k = R^{-1} W_k' F_k W_k (6x6)
   union {
     struct {
       // sweep right-hand side of stage k's states = bo[k] + na[k] + nb[k]: bo from
@@ -318,6 +320,7 @@ struct Smem {
     } fa;
   } u;
   double red[12 * N + 32];  // per-row partial reductions [12 N); [12 N, +32) sweep meeting point
+  double dump[16 * N];      // per-lane sink: predicated stores write here instead of branching
   int flag[4];
 };
 
@@ -352,12 +355,16 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
   lds_cd* Ab = (lds_cd*)sh.Ab;
   lds_cd* GHr = (lds_cd*)&sh.GH[0][0];
   lds_cd* SmR = (lds_cd*)&sh.Sm[0][0];
+  lds_cd* FWr = (lds_cd*)&sh.FWs[0][0];
+  lds_cd* QLr = (lds_cd*)&sh.QL[0][0];
   double* const gh0 = &sh.GH[0][0];
   int fo = FO<N>(k, f, cc), xo = XO<N>(k, ph);  // own force / state column in Ab
   int cr = (t >> 4) & 1;            // sweep row (wave 0): 0 top-down, 1 bottom-up
   int rr_ = s < 12 ? s : 11;        // sweep lane's state index
+  // store v at q when c holds, else into this lane's sink (branch-free)
+  auto st_if = [&](bool c_, double* q, double v) __attribute__((always_inline)) { *(c_ ? q : &sh.dump[t]) = v; };
   auto launder = [&]() __attribute__((always_inline)) {
-    asm volatile("" : "+v"(Ab), "+v"(GHr), "+v"(SmR), "+v"(k), "+v"(f), "+v"(c), "+v"(cc), "+v"(ph), "+v"(fo), "+v"(xo),
+    asm volatile("" : "+v"(Ab), "+v"(GHr), "+v"(SmR), "+v"(FWr), "+v"(QLr), "+v"(k), "+v"(f), "+v"(c), "+v"(cc), "+v"(ph), "+v"(fo), "+v"(xo),
                  "+v"(cr), "+v"(rr_));
   };
   (void)lane;
@@ -726,7 +733,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         }
         if (cl) {
 #pragma unroll
-          for (int j = 0; j < 6; ++j) gk[36 + 6 * ph + j] = fw[j];
+          for (int j = 0; j < 6; ++j) { gk[36 + 6 * ph + j] = fw[j]; sh.FWs[k][6 * ph + j] = fw[j]; }
         }
         wave_sync();
         // Q = W' (F W): 36 entries over the row's 16 lanes
@@ -738,6 +745,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           for (int psi = 0; psi < 12; ++psi)
             acc += (r1 * Bc(k, 6 + j1, psi / 3, psi % 3)) * gk[36 + 6 * psi + j2];
           gk[e] = acc;
+          sh.QL[k][e] = acc / r1;
         }
       }
       const double dgX = PbX() + sigma;
@@ -777,13 +785,13 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
                 double acc = 0.0;
 #pragma unroll
                 for (int jj = 0; jj < 12; ++jj) acc += Lt[12 * ph + jj] * St[12 * jj + ci];
-                sh.GH[k][12 * ph + ci] = acc;  // G_k = L_k S_{k-1}^{-1}
+                sh.GH[k][12 * ph + ci] = -acc;  // -G_k = -L_k S_{k-1}^{-1} (stored negated)
               }
               if (useB) {
                 double acc = 0.0;
 #pragma unroll
                 for (int jj = 0; jj < 12; ++jj) acc += Lb[12 * ph + jj] * Sb[12 * jj + ci];
-                sh.GH[k + 1][12 * ph + ci] = acc;  // H_k = L_{k+1}' U_{k+1}^{-1}
+                sh.GH[k + 1][12 * ph + ci] = -acc;  // -H_k = -L_{k+1}' U_{k+1}^{-1}
               }
             }
           }
@@ -796,11 +804,11 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               double acc = Sw[12 * ph + ci];
               if (useT) {
 #pragma unroll
-                for (int jj = 0; jj < 12; ++jj) acc -= sh.GH[k][12 * ph + jj] * Lt[12 * ci + jj];
+                for (int jj = 0; jj < 12; ++jj) acc += sh.GH[k][12 * ph + jj] * Lt[12 * ci + jj];
               }
               if (useB) {
 #pragma unroll
-                for (int jj = 0; jj < 12; ++jj) acc -= sh.GH[k + 1][12 * ph + jj] * Lb[12 * ci + jj];
+                for (int jj = 0; jj < 12; ++jj) acc += sh.GH[k + 1][12 * ph + jj] * Lb[12 * ci + jj];
               }
               Sw[12 * ph + ci] = acc;
             }
@@ -844,6 +852,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       sync_all();
       if (cl) { sh.u.it.xs[k + 1][ph] = xX; sh.u.it.bo[k][ph] = y[0]; }
       sync_all();
+      STAMP(13);
       launder();
       double* const rowred = sh.red + 12 * k;  // this row's 12 partial maxima
       {  // primal side: A x - z on the own rows
@@ -885,7 +894,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           if (s == 0) rowred[6 + e] = v;
         }
       }
+      STAMP(14);
       sync_all();
+      STAMP(15);
       // lane s of every row reduces quantity s % 12 over the N row partials, then
       // the row shares the 12 results by row_newbcast
       double qv[12];
@@ -1052,6 +1063,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       // the inner loop iterates until convergence, max_iter or a rho update.
       bool last_checked = false;
       int iter = 1;
+      int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
       for (;;) {
         if (!factor(p.sigma)) { status = MPCQ_STATUS_FACTOR_FAILED; break; }
         STAMP(2);
@@ -1066,33 +1078,29 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma unroll
           for (int j = 0; j < 3; ++j) w[j] = rho_of(j) * z[j] - y[j];
           const double bf = colF_At(w) + p.sigma * xf;  // - q, q = 0
-          double beta;
+          // u = F b_f (kept for the forces) and beta = R B u = (F W)' b_f (rows 6..11)
+          double beta, uf;
           {
-            double ball[12], uall[12];
+            double ball[12];
             gather12(bf, ball);
-            const double uf = dot12(Fr, ball);
-            gather12(uf, uall);
-            double bcu[12];
+            uf = dot12(Fr, ball);
+            double fwc[12];
+            const int jb = ph >= 6 ? ph - 6 : 0;
 #pragma unroll
-            for (int psi = 0; psi < 12; ++psi) bcu[psi] = Bc(k, ph, psi / 3, psi % 3);
-            const double bu = dot12(bcu, uall);
-            beta = rho_of(0) * bu;
+            for (int psi = 0; psi < 12; ++psi) fwc[psi] = FWr[72 * k + 6 * psi + jb];
+            beta = dot12(fwc, ball);
           }
           {
             const double wd = ph >= 6 ? w[0] - beta : w[0];  // dynamics-row w less the force Schur term
             const double bo = p.sigma * xX + Ab[xo] * wd;
             const double na = Hd(k, ph) * wd;                 // on X_k[ph], stage k-1's column ph
             const double nb = H6(k, ph) * w[0];               // on X_k[ph+6] (ph < 6)
-            if (cl) {
-              sh.u.it.bo[k][ph] = bo;
-              if (k >= 1) {
-                sh.u.it.na[k - 1][ph] = na;
-                sh.u.it.nb[k - 1][ph < 6 ? ph + 6 : ph - 6] = ph < 6 ? nb : 0.0;
-              } else {
-                sh.u.it.na[N - 1][ph] = 0.0;  // the last stage's columns have no next stage
-                sh.u.it.nb[N - 1][ph] = 0.0;
-              }
-            }
+            // stage 0 zeroes the last stage's na / nb (that stage has no next stage)
+            const bool hp = k >= 1;
+            const int kn = hp ? k - 1 : N - 1;
+            st_if(cl, &sh.u.it.bo[k][ph], bo);
+            st_if(cl, &sh.u.it.na[kn][ph], hp ? na : 0.0);
+            st_if(cl, &sh.u.it.nb[kn][hp ? (ph < 6 ? ph + 6 : ph - 6) : ph], hp && ph < 6 ? nb : 0.0);
           }
           sync_all();
           STAMP(3);
@@ -1143,13 +1151,15 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
                 yb[0] = rbc<0>(ys); yb[1] = rbc<1>(ys); yb[2] = rbc<2>(ys);
                 yb[3] = rbc<3>(ys); yb[4] = rbc<4>(ys); yb[5] = rbc<5>(ys);
               }
-              const double acc = bc - pair_sum(((gc[0] * yb[0] + gc[2] * yb[2]) + gc[4] * yb[4]) +
-                                               ((gc[1] * yb[1] + gc[3] * yb[3]) + gc[5] * yb[5]));
+              // y = b - G y_prev with -G stored: half 0 starts its chains from b
+              const double i0 = half == 0 ? bc : 0.0;
+              const double acc = pair_sum((fma(gc[4], yb[4], fma(gc[2], yb[2], fma(gc[0], yb[0], i0)))) +
+                                          (fma(gc[5], yb[5], fma(gc[3], yb[3], gc[1] * yb[1]))));
               // off the chain: w of the stage finished by the previous step
               const double wv = pair_sum(((sc[0] * yb[0] + sc[2] * yb[2]) + sc[4] * yb[4]) +
                                          ((sc[1] * yb[1] + sc[3] * yb[3]) + sc[5] * yb[5]));
               const int kp = kk_of(j - 1);
-              if ((j == 1 || act_of(j - 1)) && kp != MID && half == 0 && s < 12) sh.u.it.yv[kp][rr_] = wv;
+              st_if((j == 1 || act_of(j - 1)) && kp != MID && half == 0 && s < 12, &sh.u.it.yv[kp][rr_], wv);
               yp = act_of(j) ? acc : yp;
             }
             // meeting stage: x_m = M^{-1} (y_m + v_m - b_m)
@@ -1193,37 +1203,65 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
                 for (int i = 0; i < 6; ++i) g[i] = M[12 * i];
                 bq = sh.u.it.yv[okc_of(j + 1)][rr_];
               }
-              const double acc = bc - pair_sum(dot6(gc, half_shift(xp)));
+              double xb[6];
+              {
+                const double xs_ = half_shift(xp);
+                xb[0] = rbc<0>(xs_); xb[1] = rbc<1>(xs_); xb[2] = rbc<2>(xs_);
+                xb[3] = rbc<3>(xs_); xb[4] = rbc<4>(xs_); xb[5] = rbc<5>(xs_);
+              }
+              const double i0 = half == 0 ? bc : 0.0;  // x = w - G' x_next with -G stored
+              const double acc = pair_sum((fma(gc[4], xb[4], fma(gc[2], xb[2], fma(gc[0], xb[0], i0)))) +
+                                          (fma(gc[5], xb[5], fma(gc[3], xb[3], gc[1] * xb[1]))));
               const int kk = ok_of(j);
               const bool act = cr == 0 || kk <= N - 1;
               xp = act ? acc : xp;
-              if (act && half == 0 && s < 12) sh.u.it.xs[kk + 1][rr_] = acc;
+              st_if(act && half == 0 && s < 12, &sh.u.it.xs[kk < N ? kk + 1 : N][rr_], acc);
             }
           }
           sync_all();
           STAMP(7);
           STAMP(8);
-          // P8: forces f_k = F_k (b_f - W_k gamma_k)
-          double sf, sX;
+          // P8: forces f_k = F_k (b_f - R B' g) = u - (F W) g, with g = Xd X_{k+1} + Hd X_k
+          // on the velocity rows (the states' part of those rows)
+          double sf, sX, gm[6];
           {
             sX = sh.u.it.xs[k + 1][ph];
-            double g = Ab[xo] * sX;
-            const double g1 = g + Hd(k, ph) * sh.u.it.xs[k][ph];
-            g = (k >= 1 ? g1 : g) * rho_of(0);  // used from the lanes of rows 6..11 only
-            const double gm6 = rbc<LN(6)>(g), gm7 = rbc<LN(7)>(g), gm8 = rbc<LN(8)>(g);
-            double wg = Ab[fo] * sel3(cc, gm6, gm7, gm8);
-            wg += Ab[fo + 1] * rbc<LN(9)>(g);
-            wg += Ab[fo + 2] * rbc<LN(10)>(g);
-            wg += Ab[fo + 3] * rbc<LN(11)>(g);
-            double rall[12];
-            gather12(bf - wg, rall);
-            sf = dot12(Fr, rall);
+            const double g0 = Ab[xo] * sX;
+            const double g1 = g0 + Hd(k, ph) * sh.u.it.xs[k][ph];
+            const double g = k >= 1 ? g1 : g0;  // used from the lanes of rows 6..11 only
+            gm[0] = rbc<LN(6)>(g); gm[1] = rbc<LN(7)>(g); gm[2] = rbc<LN(8)>(g);
+            gm[3] = rbc<LN(9)>(g); gm[4] = rbc<LN(10)>(g); gm[5] = rbc<LN(11)>(g);
+            lds_cd* fwr = FWr + 72 * k + 6 * ph;
+            sf = uf - (((fwr[0] * gm[0] + fwr[2] * gm[2]) + fwr[4] * gm[4]) +
+                       ((fwr[1] * gm[1] + fwr[3] * gm[3]) + fwr[5] * gm[5]));
           }
           STAMP(9);
-          // P9: z, y update (osqp update_z / update_y), x update
+          // P9: z, y update (osqp update_z / update_y), x update.  A x~ on the own rows:
+          // dynamics rows use B f = B u - B F W g = beta / rho - (R^{-1} Q) g (no force gather)
           {
             double ax[3];
-            row_A(sf, sX, ax);
+            {
+              const double* xp = sh.u.it.xs[k];
+              const double xa = xp[ph], xb = xp[ph < 6 ? ph + 6 : ph];
+              double dyn = Ab[xo] * sX;
+              const double d1 = dyn + Hd(k, ph) * xa;
+              const double d2 = d1 + H6(k, ph) * xb;
+              dyn = k >= 1 ? (ph < 6 ? d2 : d1) : dyn;
+              lds_cd* ql = QLr + 36 * k + 6 * (ph >= 6 ? ph - 6 : 0);
+              const double bfv = beta * rinv_of(0) - (((ql[0] * gm[0] + ql[2] * gm[2]) + ql[4] * gm[4]) +
+                                                      ((ql[1] * gm[1] + ql[3] * gm[3]) + ql[5] * gm[5]));
+              dyn = ph >= 6 ? dyn + bfv : dyn;
+              // friction rows: lane c < 3 owns row c, lane 3 rows 3 and 4 (all loads unconditional)
+              const double q0 = qbc<0>(sf), q1 = qbc<1>(sf), q2 = qbc<2>(sf);
+              const int ta = cl ? c : 3;
+              const double frA = Ab[FO<N>(k, f, 2) + 5 + ta] * q2 +
+                                 Ab[FO<N>(k, f, ta >> 1) + 5 + (ta & 1)] * ((ta >> 1) == 0 ? q0 : q1);
+              const double frB = Ab[FO<N>(k, f, 2) + 9] * q2;
+              const double swg = Ab[fo + 4] * sf;
+              ax[0] = cl ? dyn : frA;
+              ax[1] = cl ? swg : frB;
+              ax[2] = cl ? frA : 0.0;
+            }
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
               const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
@@ -1237,9 +1275,11 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             xX = p.alpha * sX + (1.0 - p.alpha) * xX;
           }
           STAMP(10);
-          const bool can_check = p.check_termination > 0 && (iter % p.check_termination == 0);
-          const bool adapt = p.adaptive_rho && p.adaptive_rho_interval > 0 &&
-                             (iter % p.adaptive_rho_interval == 0);
+          // iter % check_termination == 0 / iter % adaptive_rho_interval == 0, by countdown
+          const bool can_check = p.check_termination > 0 && --to_check == 0;
+          if (can_check) to_check = p.check_termination;
+          const bool adapt = p.adaptive_rho && p.adaptive_rho_interval > 0 && --to_adapt == 0;
+          if (adapt) to_adapt = p.adaptive_rho_interval;
           last_checked = can_check;
           if (can_check || adapt) {
             update_info();

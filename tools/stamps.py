@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(REPO, "mpc-tsid_amd"))
 os.environ.setdefault("MPCQ_LIB_VARIANT", "stamps")
 
 NAMES = ["prologue", "scaling", "factor", "iter:w,b,u,beta,bt", "-", "-", "iter:inward sweeps+S^-1 y",
-         "iter:outward sweeps", "-", "iter:forces", "iter:z/y/x update", "iter:check+adapt", "epilogue"]
+         "iter:outward sweeps", "-", "iter:forces", "iter:z/y/x update", "iter:check+adapt", "epilogue", "chk:sync", "chk:resid", "chk:barrier"]
 
 
 def main():
@@ -38,7 +38,7 @@ def main():
     torch.cuda.synchronize()
     S = stamps.cpu().numpy().astype(np.float64)
     its = it.cpu().numpy()
-    tot = S[:, :len(NAMES)].sum(axis=1)
+    tot = S[:, :13].sum(axis=1)
     print(f"batch {a.batch} N={a.N}: iters median {np.median(its)} max {its.max()}; "
           f"kernel ms (event) {eng.last_kernel_ms()[1]:.2f}")
     print(f"cycles per instance: median {np.median(tot):.3e}; per iteration {np.median(tot / its):.0f}")

@@ -41,6 +41,7 @@ namespace {
 // an empty asm so the compiler re-reads LDS instead of hoisting dozens of
 // invariant values into registers.
 typedef __attribute__((address_space(3))) const double lds_cd;
+typedef __attribute__((address_space(3))) double lds_d;
 
 constexpr double kInf = 1e30;  // OSQP_INFTY
 constexpr double kMinScaling = 1e-4, kMaxScaling = 1e4;
@@ -645,34 +646,62 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     // dynamics-row rho of stage kk (published in GH[kk][108..120) at factor time)
     auto rdy = [&](int kk, int i) __attribute__((always_inline)) { return GHr[144 * kk + 108 + i]; };
     auto Qv = [&](int kk, int j1, int j2) __attribute__((always_inline)) { return GHr[144 * kk + 6 * j1 + j2]; };
-    // entry (jr, ic) of L_kk: dynamics rows of stage kk on (X_{kk+1}[jr], X_kk[ic]), kk >= 1
-    auto Lval = [&](int kk, int jr, int ic) __attribute__((always_inline)) -> double {
-      double v = 0.0;
-      if (ic == jr) v = rdy(kk, jr) * Xd(kk, jr) * Hd(kk, jr);
-      if (jr < 6 && ic == jr + 6) v = rdy(kk, jr) * Xd(kk, jr) * H6(kk, jr);
-      if (jr >= 6 && ic >= 6) v -= Xd(kk, jr) * Qv(kk, jr - 6, ic - 6) * Hd(kk, ic);
-      return v;
-    };
-    // row i of D_kk (state block of X_{kk+1})
-    auto Drow = [&](int kk, int i, double diag0, double (&Dr)[12]) __attribute__((always_inline)) {
-      const double Xdi = Xd(kk, i);
-      double dg = diag0 + rdy(kk, i) * Xdi * Xdi;
-      double h1 = 0.0, h6 = 0.0;
-      if (kk < N - 1) {
-        h1 = Hd(kk + 1, i);
-        dg += rdy(kk + 1, i) * h1 * h1;
-        if (i >= 6) { h6 = H6(kk + 1, i - 6); dg += rdy(kk + 1, i - 6) * h6 * h6; }
+    // The factorisation's row builders are branch-free: every load is unconditional
+    // (indices clamped in range) and the structure is applied by selects.
+    // Row i of L_kk (kk >= 1): the dynamics rows of stage kk on (X_{kk+1}[i], X_kk[ci]).
+    auto Ctop = [&](int kk, int i, double (&Cr)[12]) __attribute__((always_inline)) {
+      const int iq = i >= 6 ? i - 6 : 0;
+      const double ri = rdy(kk, i), xi = Xd(kk, i), hi = Hd(kk, i), h6 = H6(kk, i < 6 ? i : 0);
+      const double dv = ri * xi * hi, tv = ri * xi * h6;
+#pragma unroll
+      for (int ci = 0; ci < 12; ++ci) {
+        double v = (ci == i) ? dv : 0.0;
+        v = (i < 6 && ci == i + 6) ? tv : v;
+        if (ci >= 6) {
+          const double sc = xi * Qv(kk, iq, ci - 6) * Hd(kk, ci);
+          v = i >= 6 ? v - sc : v;
+        }
+        Cr[ci] = v;
       }
+    };
+    // Column i of L_kk (kk >= 1), i.e. row i of L_kk'.
+    auto Cbot = [&](int kk, int i, double (&Cr)[12]) __attribute__((always_inline)) {
+      const int ip = i >= 6 ? i - 6 : 0;
+      const double hi = Hd(kk, i);
+      const double dv = rdy(kk, i) * Xd(kk, i) * hi;
+      const double tv = rdy(kk, ip) * Xd(kk, ip) * H6(kk, ip);
+#pragma unroll
+      for (int jr = 0; jr < 12; ++jr) {
+        double v = (jr == i) ? dv : 0.0;
+        v = (i >= 6 && jr == i - 6) ? tv : v;
+        if (jr >= 6) {
+          const double sc = Xd(kk, jr) * Qv(kk, jr - 6, ip) * hi;
+          v = i >= 6 ? v - sc : v;
+        }
+        Cr[jr] = v;
+      }
+    };
+    // Row i of D_kk (the state block of X_{kk+1}).
+    auto Drow = [&](int kk, int i, double diag0, double (&Dr)[12]) __attribute__((always_inline)) {
+      const bool nx = kk < N - 1;  // stage kk+1 exists
+      const int k1 = nx ? kk + 1 : kk;
+      const int i6 = i < 6 ? i : i - 6, iq = i >= 6 ? i - 6 : 0;
+      const double xi = Xd(kk, i), ri0 = rdy(kk, i);
+      const double hi1 = Hd(k1, i), ri1 = rdy(k1, i);
+      const double h6p = H6(k1, i6), rp1 = rdy(k1, i6), hp1 = Hd(k1, i6);
+      double dg = diag0 + ri0 * xi * xi;
+      const double dn = ri1 * hi1 * hi1 + (i >= 6 ? rp1 * h6p * h6p : 0.0);
+      dg = nx ? dg + dn : dg;
+      const double cross = nx ? (i < 6 ? ri1 * hi1 * h6p : rp1 * hp1 * h6p) : 0.0;
+      const int partner = i < 6 ? i + 6 : i - 6;
 #pragma unroll
       for (int ci = 0; ci < 12; ++ci) {
         double v = (ci == i) ? dg : 0.0;
-        if (kk < N - 1) {
-          if (i < 6 && ci == i + 6) v = rdy(kk + 1, i) * h1 * H6(kk + 1, i);
-          if (i >= 6 && ci == i - 6) v = rdy(kk + 1, ci) * Hd(kk + 1, ci) * h6;
-        }
-        if (i >= 6 && ci >= 6) {
-          v -= Xdi * Qv(kk, i - 6, ci - 6) * Xd(kk, ci);
-          if (kk < N - 1) v -= h1 * Qv(kk + 1, i - 6, ci - 6) * Hd(kk + 1, ci);
+        v = (ci == partner) ? cross : v;
+        if (ci >= 6) {
+          const double s0 = xi * Qv(kk, iq, ci - 6) * Xd(kk, ci);
+          const double s1 = hi1 * Qv(k1, iq, ci - 6) * Hd(k1, ci);
+          v = i >= 6 ? v - (nx ? s0 + s1 : s0) : v;
         }
         Dr[ci] = v;
       }
@@ -750,6 +779,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       }
       const double dgX = PbX() + sigma;
       sync_all();
+      STAMP(13);
       // ---- phase S: two-ended block factorisation of the state system.  Per
       // step the active row keeps one 12-vector live (its row of S / U / M):
       // L goes to LDS entry by entry, G / H straight to their GH slot.
@@ -760,6 +790,49 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       // Step j < MID: top row k = j (C = L_k against S_{k-1}^{-1}) and bottom row
       // k = N-1-j > MID (C = L_{k+1}' against U_{k+1}^{-1}) in parallel; step MID:
       // the meeting row (both couplings).  G_k -> GH[k], H_k -> GH[k+1], M^{-1} -> GH[0].
+      // One coupling of the active row: upper C = L_k (row ph) against S_{k-1}^{-1}
+      // (St), giving G_k -> GH[k]; lower C = L_{k+1}' (row ph) against U_{k+1}^{-1}
+      // (Sb), giving H_k -> GH[k+1].  Ro -= (C S^{-1}) C'.  Products run block by
+      // block (a compiler fence per block keeps the loads from piling up).
+      auto couple = [&](bool upper, double (&Ro)[12]) __attribute__((always_inline)) {
+        double Cr[12];
+        if (upper) Ctop(k, ph, Cr);
+        else Cbot(k + 1, ph, Cr);
+        double* const Cb = upper ? Lt : Lb;
+        const double* const Sp = upper ? St : Sb;
+        if (cl) {
+#pragma unroll
+          for (int ci = 0; ci < 12; ++ci) Cb[12 * ph + ci] = Cr[ci];
+        }
+        wave_sync();  // C rows visible (and this row's reads of GH[k], GH[k+1] are done)
+        double G[12];
+#pragma unroll
+        for (int ci = 0; ci < 12; ++ci) G[ci] = 0.0;
+#pragma unroll
+        for (int jj = 0; jj < 12; ++jj) {
+#pragma unroll
+          for (int ci = 0; ci < 12; ++ci) G[ci] = fma(Cr[jj], Sp[12 * jj + ci], G[ci]);
+          asm volatile("" ::: "memory");
+        }
+        if (cl) {
+          double* const Gd = &sh.GH[upper ? k : k + 1][12 * ph];
+#pragma unroll
+          for (int ci = 0; ci < 12; ++ci) Gd[ci] = -G[ci];  // stored negated
+        }
+#pragma unroll
+        for (int ci = 0; ci < 12; ++ci) {
+          double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+          for (int jj = 0; jj < 12; jj += 2) {
+            a0 = fma(G[jj], Cb[12 * ci + jj], a0);
+            a1 = fma(G[jj + 1], Cb[12 * ci + jj + 1], a1);
+          }
+          Ro[ci] -= a0 + a1;
+          asm volatile("" ::: "memory");
+        }
+      };
+      // Step j < MID: top row k = j and bottom row k = N-1-j > MID in parallel; step
+      // MID: the meeting row (both couplings).  M^{-1} -> GH[0].
 #pragma nounroll
       for (int j = 0; j <= MID; ++j) {
         launder();
@@ -767,69 +840,25 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         const bool top = !mid && k == j, bot = !mid && k == N - 1 - j && k > MID, mrow = mid && k == MID;
         if (top || bot || mrow) {
           const bool useT = (top && k > 0) || mrow, useB = (bot && k < N - 1) || mrow;
-          double* const Sw = bot ? Sb : St;  // holds the previous inverse, then this row's block
           double Ro[12];
-          Drow(k, ph, dgX, Ro);  // every read of GH[k], GH[k+1] by this row happens here ...
-          if (cl) {
-#pragma unroll 1
-            for (int ci = 0; ci < 12; ++ci) {
-              if (useT) Lt[12 * ph + ci] = Lval(k, ph, ci);
-              if (useB) Lb[12 * ph + ci] = Lval(k + 1, ci, ph);
-            }
-          }
-          wave_sync();  // ... and here, so G / H may now overwrite those slots
-          if (cl) {
-#pragma unroll 1
-            for (int ci = 0; ci < 12; ++ci) {
-              if (useT) {
-                double acc = 0.0;
-#pragma unroll
-                for (int jj = 0; jj < 12; ++jj) acc += Lt[12 * ph + jj] * St[12 * jj + ci];
-                sh.GH[k][12 * ph + ci] = -acc;  // -G_k = -L_k S_{k-1}^{-1} (stored negated)
-              }
-              if (useB) {
-                double acc = 0.0;
-#pragma unroll
-                for (int jj = 0; jj < 12; ++jj) acc += Lb[12 * ph + jj] * Sb[12 * jj + ci];
-                sh.GH[k + 1][12 * ph + ci] = -acc;  // -H_k = -L_{k+1}' U_{k+1}^{-1}
-              }
-            }
-          }
-          wave_sync();  // the previous inverse is consumed: Sw takes this row's block
-          if (cl) {
-#pragma unroll
-            for (int ci = 0; ci < 12; ++ci) Sw[12 * ph + ci] = Ro[ci];
-#pragma unroll 1
-            for (int ci = 0; ci < 12; ++ci) {
-              double acc = Sw[12 * ph + ci];
-              if (useT) {
-#pragma unroll
-                for (int jj = 0; jj < 12; ++jj) acc += sh.GH[k][12 * ph + jj] * Lt[12 * ci + jj];
-              }
-              if (useB) {
-#pragma unroll
-                for (int jj = 0; jj < 12; ++jj) acc += sh.GH[k + 1][12 * ph + jj] * Lb[12 * ci + jj];
-              }
-              Sw[12 * ph + ci] = acc;
-            }
-          }
-          wave_sync();
-#pragma unroll
-          for (int ci = 0; ci < 12; ++ci) Ro[ci] = Sw[12 * ph + ci];
+          Drow(k, ph, dgX, Ro);  // reads GH[k], GH[k+1] (Q, rho) before any G / H lands there
+          if (useT) couple(true, Ro);
+          if (useB) couple(false, Ro);
           gj12(Ro, ph, ok);
           if (cl) {
 #pragma unroll
             for (int ci = 0; ci < 12; ++ci) sh.Sm[k][12 * ph + ci] = Ro[ci];
           }
-          wave_sync();
+          wave_sync();  // the previous inverse has been consumed by this row
           if (cl) {
-            double* dst = mrow ? &sh.GH[0][0] : Sw;
+            double* dst = mrow ? &sh.GH[0][0] : (bot ? Sb : St);
 #pragma unroll
             for (int ci = 0; ci < 12; ++ci) dst[12 * ph + ci] = Ro[ci];
           }
         }
         sync_all();
       }
+      STAMP(14);
       // a non-positive pivot anywhere fails the whole instance (uniform result)
       if (!ok) atomicOr(&sh.flag[2], 1);
       sync_all();
@@ -852,7 +881,6 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       sync_all();
       if (cl) { sh.u.it.xs[k + 1][ph] = xX; sh.u.it.bo[k][ph] = y[0]; }
       sync_all();
-      STAMP(13);
       launder();
       double* const rowred = sh.red + 12 * k;  // this row's 12 partial maxima
       {  // primal side: A x - z on the own rows
@@ -894,9 +922,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           if (s == 0) rowred[6 + e] = v;
         }
       }
-      STAMP(14);
       sync_all();
-      STAMP(15);
       // lane s of every row reduces quantity s % 12 over the N row partials, then
       // the row shares the 12 results by row_newbcast
       double qv[12];
@@ -1115,35 +1141,40 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           // the outward sweeps.
           const int half = (t >> 5) & 1, hoff = 6 * half;
           if (t < 64) {
-            // inward step j: top kk = j (G_kk in GH[kk]); bottom kk = N-1-j (H_kk in GH[kk+1])
-            auto kk_of = [&](int j) __attribute__((always_inline)) { return cr == 0 ? j : N - 1 - j; };
-            auto slot_of = [&](int j) __attribute__((always_inline)) { return cr == 0 ? j : N - j; };
-            auto act_of = [&](int j) __attribute__((always_inline)) { return cr == 0 || kk_of(j) >= MID; };
-            auto bt_of = [&](int kk) __attribute__((always_inline)) {
-              return (sh.u.it.bo[kk][rr_] + sh.u.it.na[kk][rr_]) + sh.u.it.nb[kk][rr_];
+            // Inward step j: top kk = j (G_kk in GH[kk]), bottom kk = N-1-j (H_kk in
+            // GH[kk+1]).  Pointers walk the stages (+-1 slot per step); the asm keeps
+            // them in registers so each step's loads stay in that step.
+            const int gs = cr == 0 ? 144 : -144, bs = cr == 0 ? 12 : -12;
+            lds_cd* GpN = GHr + 144 * (cr == 0 ? 1 : N - 1) + 12 * rr_ + hoff;  // G / H of step 1
+            lds_cd* SpN = SmR + 144 * (cr == 0 ? 0 : N - 1) + 12 * rr_ + hoff;  // S^{-1} of stage kk(0)
+            lds_cd* BpN = (lds_cd*)&sh.u.it.bo[cr == 0 ? 0 : N - 1][rr_];        // bo; na, nb at +12N, +24N
+            lds_d* Yp = (lds_d*)&sh.u.it.yv[cr == 0 ? 0 : N - 1][rr_];
+            auto bt_at = [&](lds_cd* q) __attribute__((always_inline)) {
+              return (q[0] + q[12 * N]) + q[24 * N];
             };
-            double yp = bt_of(kk_of(0));
+            double yp = bt_at(BpN);
+            BpN += bs;
             double g[6], sv[6], bq;
-            {
-              lds_cd* M = GHr + 144 * slot_of(1) + 12 * rr_ + hoff;
-              lds_cd* S = SmR + 144 * kk_of(0) + 12 * rr_ + hoff;
 #pragma unroll
-              for (int i = 0; i < 6; ++i) { g[i] = M[i]; sv[i] = S[i]; }
-              bq = bt_of(kk_of(1));
-            }
+            for (int i = 0; i < 6; ++i) { g[i] = GpN[i]; sv[i] = SpN[i]; }
+            GpN += gs;
+            SpN += gs;
+            bq = bt_at(BpN);
+            BpN += bs;
 #pragma unroll
             for (int j = 1; j <= MID; ++j) {
-              launder();
+              asm volatile("" : "+v"(GpN), "+v"(SpN), "+v"(BpN), "+v"(Yp));
               double gc[6], sc[6];
 #pragma unroll
               for (int i = 0; i < 6; ++i) { gc[i] = g[i]; sc[i] = sv[i]; }
               const double bc = bq;
               if (j < MID) {  // prefetch the next step's half rows and right-hand side
-                lds_cd* M = GHr + 144 * slot_of(j + 1) + 12 * rr_ + hoff;
-                lds_cd* S = SmR + 144 * kk_of(j) + 12 * rr_ + hoff;
 #pragma unroll
-                for (int i = 0; i < 6; ++i) { g[i] = M[i]; sv[i] = S[i]; }
-                bq = bt_of(kk_of(j + 1));
+                for (int i = 0; i < 6; ++i) { g[i] = GpN[i]; sv[i] = SpN[i]; }
+                GpN += gs;
+                SpN += gs;
+                bq = bt_at(BpN);
+                BpN += bs;
               }
               double yb[6];
               {
@@ -1155,19 +1186,21 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               const double i0 = half == 0 ? bc : 0.0;
               const double acc = pair_sum((fma(gc[4], yb[4], fma(gc[2], yb[2], fma(gc[0], yb[0], i0)))) +
                                           (fma(gc[5], yb[5], fma(gc[3], yb[3], gc[1] * yb[1]))));
-              // off the chain: w of the stage finished by the previous step
+              // off the chain: w of the stage the previous step finished (kk(j-1))
               const double wv = pair_sum(((sc[0] * yb[0] + sc[2] * yb[2]) + sc[4] * yb[4]) +
                                          ((sc[1] * yb[1] + sc[3] * yb[3]) + sc[5] * yb[5]));
-              const int kp = kk_of(j - 1);
-              st_if((j == 1 || act_of(j - 1)) && kp != MID && half == 0 && s < 12, &sh.u.it.yv[kp][rr_], wv);
-              yp = act_of(j) ? acc : yp;
+              const bool wok = (cr == 0 || j == 1 || N - j >= MID) && (cr == 0 ? j - 1 : N - j) != MID;
+              *(wok && half == 0 && s < 12 ? Yp : (lds_d*)&sh.dump[t]) = wv;
+              Yp += bs;
+              yp = (cr == 0 || N - 1 - j >= MID) ? acc : yp;
             }
             // meeting stage: x_m = M^{-1} (y_m + v_m - b_m)
             if (half == 0) sh.red[RMID + 16 * cr + s] = yp;
             wave_sync();
             double xp;
             {
-              const double cm = sh.red[RMID + rr_] + sh.red[RMID + 16 + rr_] - bt_of(MID);
+              const double cm = sh.red[RMID + rr_] + sh.red[RMID + 16 + rr_] -
+                                bt_at((lds_cd*)&sh.u.it.bo[MID][rr_]);
               double gm[6];
 #pragma unroll
               for (int i = 0; i < 6; ++i) gm[i] = GHr[12 * rr_ + hoff + i];
@@ -1175,33 +1208,33 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               if (cr == 0 && half == 0 && s < 12) sh.u.it.xs[MID + 1][rr_] = xp;
             }
             STAMP(6);
-            // outward step j: top kk = MID-j (G_{kk+1}' from GH[kk+1]); bottom kk = MID+j
-            // (H_{kk-1}' from GH[kk]); matrices read by column
-            auto ok_of = [&](int j) __attribute__((always_inline)) { return cr == 0 ? MID - j : MID + j; };
-            auto okc_of = [&](int j) __attribute__((always_inline)) {
-              const int kk = ok_of(j);
-              return kk <= N - 1 ? kk : N - 1;
-            };
-            auto oslot_of = [&](int j) __attribute__((always_inline)) { return cr == 0 ? MID - j + 1 : okc_of(j); };
-            {
-              lds_cd* M = GHr + 144 * oslot_of(1) + rr_ + 12 * hoff;
+            // Outward step j: top kk = MID-j (G_{kk+1}' from GH[kk+1]), bottom kk = MID+j
+            // (H_{kk-1}' from GH[kk]); matrices read by column.  The bottom row's last
+            // step (kk = N) is idle: its loads stay inside the shared memory block and
+            // its store goes to the lane's sink.
+            const int ms = cr == 0 ? -144 : 144, ws = cr == 0 ? -12 : 12;
+            lds_cd* MpN = GHr + 144 * (cr == 0 ? MID : MID + 1) + rr_ + 12 * hoff;
+            lds_cd* WpN = (lds_cd*)&sh.u.it.yv[cr == 0 ? MID - 1 : MID + 1][rr_];
+            lds_d* Xp = (lds_d*)&sh.u.it.xs[cr == 0 ? MID : MID + 2][rr_];
 #pragma unroll
-              for (int i = 0; i < 6; ++i) g[i] = M[12 * i];
-            }
+            for (int i = 0; i < 6; ++i) g[i] = MpN[12 * i];
+            MpN += ms;
             wave_sync();  // the w written by the inward rows
-            bq = sh.u.it.yv[okc_of(1)][rr_];
+            bq = WpN[0];
+            WpN += ws;
 #pragma unroll
             for (int j = 1; j <= MID; ++j) {
-              launder();
+              asm volatile("" : "+v"(MpN), "+v"(WpN), "+v"(Xp));
               double gc[6];
 #pragma unroll
               for (int i = 0; i < 6; ++i) gc[i] = g[i];
               const double bc = bq;
               if (j < MID) {
-                lds_cd* M = GHr + 144 * oslot_of(j + 1) + rr_ + 12 * hoff;
 #pragma unroll
-                for (int i = 0; i < 6; ++i) g[i] = M[12 * i];
-                bq = sh.u.it.yv[okc_of(j + 1)][rr_];
+                for (int i = 0; i < 6; ++i) g[i] = MpN[12 * i];
+                MpN += ms;
+                bq = WpN[0];
+                WpN += ws;
               }
               double xb[6];
               {
@@ -1212,10 +1245,10 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               const double i0 = half == 0 ? bc : 0.0;  // x = w - G' x_next with -G stored
               const double acc = pair_sum((fma(gc[4], xb[4], fma(gc[2], xb[2], fma(gc[0], xb[0], i0)))) +
                                           (fma(gc[5], xb[5], fma(gc[3], xb[3], gc[1] * xb[1]))));
-              const int kk = ok_of(j);
-              const bool act = cr == 0 || kk <= N - 1;
+              const bool act = cr == 0 || MID + j <= N - 1;
               xp = act ? acc : xp;
-              st_if(act && half == 0 && s < 12, &sh.u.it.xs[kk < N ? kk + 1 : N][rr_], acc);
+              *(act && half == 0 && s < 12 ? Xp : (lds_d*)&sh.dump[t]) = acc;
+              Xp += ws;
             }
           }
           sync_all();

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(REPO, "mpc-tsid_amd"))
 os.environ.setdefault("MPCQ_LIB_VARIANT", "stamps")
 
 NAMES = ["prologue", "scaling", "factor", "iter:w,b,u,beta,bt", "-", "-", "iter:inward sweeps+S^-1 y",
-         "iter:outward sweeps", "-", "iter:forces", "iter:z/y/x update", "iter:check+adapt", "epilogue", "chk:sync", "chk:resid", "chk:barrier"]
+         "iter:outward sweeps", "-", "iter:forces", "iter:z/y/x update", "iter:check+adapt", "epilogue", "fac:phaseP", "fac:phaseS"]
 
 
 def main():

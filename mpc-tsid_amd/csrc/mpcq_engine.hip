@@ -556,11 +556,18 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 
     // per-row rho / 1/rho from the row's class and the (uniform) rho values
     double r_in = 0.0, r_eq = 0.0, ri_in = 0.0, ri_eq = 0.0;
+    double rr[3], ri[3];  // per-row rho and 1/rho (refreshed with rho)
     auto set_rho = [&]() __attribute__((always_inline)) {
       r_in = uni(rho_s);
       r_eq = uni(kRhoEq * rho_s);
       ri_in = uni(1.0 / r_in);
       ri_eq = uni(1.0 / r_eq);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const unsigned cj = (cls >> (2 * j)) & 3u;
+        rr[j] = cj == RC_EQ ? r_eq : (cj == RC_INEQ ? r_in : kRhoMin);
+        ri[j] = cj == RC_EQ ? ri_eq : (cj == RC_INEQ ? ri_in : 1.0 / kRhoMin);
+      }
     };
     auto rho_of = [&](int j) __attribute__((always_inline)) -> double {
       const unsigned cj = (cls >> (2 * j)) & 3u;
@@ -1090,20 +1097,61 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       bool last_checked = false;
       int iter = 1;
       int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
+      // per-lane constants of the ADMM loop: LDS offsets, flags, scaled bounds
+      const bool hp = k >= 1, isv = ph >= 6;
+      const int oXd = xo;                                                // Xd(k, ph)
+      const int oHd = XO<N>(hp ? k - 1 : 0, ph) + (ph < 6 ? 1 : 2);      // Hd(k, ph)
+      const int oH6 = XO<N>(hp ? k - 1 : 0, ph < 6 ? ph + 6 : 11) + 1;   // H6(k, ph)
+      const int oF = fo;
+      const int ta = cl ? c : 3;  // first own friction row
+      const bool ta0 = (ta >> 1) == 0;
+      const int oFa = FO<N>(k, f, ta >> 1) + 5 + (ta & 1), oFb = FO<N>(k, f, 2) + 5 + ta;
+      const int oF4 = FO<N>(k, f, 2) + 9;
+      const int oFW = 72 * k + 6 * ph, oFWc = 72 * k + (isv ? ph - 6 : 0);
+      const int oQL = 36 * k + 6 * (isv ? ph - 6 : 0);
+      const int oXS = 12 * (k + 1) + ph, oXSp = 12 * k + ph, oXSp6 = 12 * k + (ph < 6 ? ph + 6 : ph);
+      const double m2 = cc == 2 ? 1.0 : 0.0;
+      lds_cd* XSr = (lds_cd*)&sh.u.it.xs[0][0];
+      double* const Wbo = &sh.u.it.bo[k][ph];
+      double* const Wna = &sh.u.it.na[hp ? k - 1 : N - 1][ph];
+      double* const Wnb = &sh.u.it.nb[hp ? k - 1 : N - 1][hp ? (ph < 6 ? ph + 6 : ph - 6) : ph];
+      double* const Wdump = &sh.dump[t];
+      double lo[3], hi[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) { lo[j] = lo_of(j); hi[j] = hi_of(j); }
+      auto launder_p = [&]() __attribute__((always_inline)) {
+        asm volatile("" : "+v"(Ab), "+v"(GHr), "+v"(SmR), "+v"(FWr), "+v"(QLr), "+v"(XSr));
+      };
       for (;;) {
         if (!factor(p.sigma)) { status = MPCQ_STATUS_FACTOR_FAILED; break; }
         STAMP(2);
         bool refactor = false;
         for (; iter <= p.max_iter; ++iter) {
-          launder();
+          launder_p();
           // P1-P4: w = rho z - y; b_f = sigma x_f + A_f' w and u = F b_f, beta = R B u
           // (stage-local, DPP only); then the sweep right-hand side of the own state
           // column (bo) and this stage's dynamics-row terms of stage k-1's state
           // columns (na, nb): the only LDS hand-off before the sweeps.
           double w[3];
 #pragma unroll
-          for (int j = 0; j < 3; ++j) w[j] = rho_of(j) * z[j] - y[j];
-          const double bf = colF_At(w) + p.sigma * xf;  // - q, q = 0
+          for (int j = 0; j < 3; ++j) w[j] = rr[j] * z[j] - y[j];
+          double bf;
+          {  // force column of A' w: dynamics rows 6..11 (row broadcast), swing, friction (quad)
+            const double w6 = rbc<LN(6)>(w[0]), w7 = rbc<LN(7)>(w[0]), w8 = rbc<LN(8)>(w[0]);
+            const double w9 = rbc<LN(9)>(w[0]), w10 = rbc<LN(10)>(w[0]), w11 = rbc<LN(11)>(w[0]);
+            const double wf0 = qbc<0>(w[2]), wf1 = qbc<1>(w[2]), wf2 = qbc<2>(w[2]);
+            const double wf3 = qbc<3>(w[0]), wf4 = qbc<3>(w[1]);
+            lds_cd* A = Ab + oF;
+            double sA = A[0] * (cc == 0 ? w6 : (cc == 1 ? w7 : w8));
+            double sB = A[1] * w9;
+            sA += A[2] * w10;
+            sB += A[3] * w11;
+            sA += A[4] * w[1];
+            sB += A[5] * (cc == 1 ? wf2 : wf0);
+            sA += A[6] * (cc == 1 ? wf3 : wf1);
+            const double sC = (A[7] * wf2 + A[8] * wf3) + A[9] * wf4;  // friction rows 2..4 (cc == 2)
+            bf = ((sA + sB) + m2 * sC) + p.sigma * xf;                 // - q, q = 0
+          }
           // u = F b_f (kept for the forces) and beta = R B u = (F W)' b_f (rows 6..11)
           double beta, uf;
           {
@@ -1111,22 +1159,19 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             gather12(bf, ball);
             uf = dot12(Fr, ball);
             double fwc[12];
-            const int jb = ph >= 6 ? ph - 6 : 0;
 #pragma unroll
-            for (int psi = 0; psi < 12; ++psi) fwc[psi] = FWr[72 * k + 6 * psi + jb];
+            for (int psi = 0; psi < 12; ++psi) fwc[psi] = FWr[oFWc + 6 * psi];
             beta = dot12(fwc, ball);
           }
           {
-            const double wd = ph >= 6 ? w[0] - beta : w[0];  // dynamics-row w less the force Schur term
-            const double bo = p.sigma * xX + Ab[xo] * wd;
-            const double na = Hd(k, ph) * wd;                 // on X_k[ph], stage k-1's column ph
-            const double nb = H6(k, ph) * w[0];               // on X_k[ph+6] (ph < 6)
+            const double wd = isv ? w[0] - beta : w[0];  // dynamics-row w less the force Schur term
+            const double bo = p.sigma * xX + Ab[oXd] * wd;
+            const double na = Ab[oHd] * wd;              // Hd(k, ph): on X_k[ph], stage k-1's column ph
+            const double nb = Ab[oH6] * w[0];            // H6(k, ph): on X_k[ph+6] (ph < 6)
             // stage 0 zeroes the last stage's na / nb (that stage has no next stage)
-            const bool hp = k >= 1;
-            const int kn = hp ? k - 1 : N - 1;
-            st_if(cl, &sh.u.it.bo[k][ph], bo);
-            st_if(cl, &sh.u.it.na[kn][ph], hp ? na : 0.0);
-            st_if(cl, &sh.u.it.nb[kn][hp ? (ph < 6 ? ph + 6 : ph - 6) : ph], hp && ph < 6 ? nb : 0.0);
+            *(cl ? Wbo : Wdump) = bo;
+            *(cl ? Wna : Wdump) = hp ? na : 0.0;
+            *(cl ? Wnb : Wdump) = hp && !isv ? nb : 0.0;
           }
           sync_all();
           STAMP(3);
@@ -1257,14 +1302,15 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           // P8: forces f_k = F_k (b_f - R B' g) = u - (F W) g, with g = Xd X_{k+1} + Hd X_k
           // on the velocity rows (the states' part of those rows)
           double sf, sX, gm[6];
+          const double xa = XSr[oXSp], xb = XSr[oXSp6];
           {
-            sX = sh.u.it.xs[k + 1][ph];
-            const double g0 = Ab[xo] * sX;
-            const double g1 = g0 + Hd(k, ph) * sh.u.it.xs[k][ph];
-            const double g = k >= 1 ? g1 : g0;  // used from the lanes of rows 6..11 only
+            sX = XSr[oXS];
+            const double g0 = Ab[oXd] * sX;
+            const double g1 = g0 + Ab[oHd] * xa;
+            const double g = hp ? g1 : g0;  // used from the lanes of rows 6..11 only
             gm[0] = rbc<LN(6)>(g); gm[1] = rbc<LN(7)>(g); gm[2] = rbc<LN(8)>(g);
             gm[3] = rbc<LN(9)>(g); gm[4] = rbc<LN(10)>(g); gm[5] = rbc<LN(11)>(g);
-            lds_cd* fwr = FWr + 72 * k + 6 * ph;
+            lds_cd* fwr = FWr + oFW;
             sf = uf - (((fwr[0] * gm[0] + fwr[2] * gm[2]) + fwr[4] * gm[4]) +
                        ((fwr[1] * gm[1] + fwr[3] * gm[3]) + fwr[5] * gm[5]));
           }
@@ -1274,23 +1320,19 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           {
             double ax[3];
             {
-              const double* xp = sh.u.it.xs[k];
-              const double xa = xp[ph], xb = xp[ph < 6 ? ph + 6 : ph];
-              double dyn = Ab[xo] * sX;
-              const double d1 = dyn + Hd(k, ph) * xa;
-              const double d2 = d1 + H6(k, ph) * xb;
-              dyn = k >= 1 ? (ph < 6 ? d2 : d1) : dyn;
-              lds_cd* ql = QLr + 36 * k + 6 * (ph >= 6 ? ph - 6 : 0);
-              const double bfv = beta * rinv_of(0) - (((ql[0] * gm[0] + ql[2] * gm[2]) + ql[4] * gm[4]) +
-                                                      ((ql[1] * gm[1] + ql[3] * gm[3]) + ql[5] * gm[5]));
-              dyn = ph >= 6 ? dyn + bfv : dyn;
+              double dyn = Ab[oXd] * sX;
+              const double d1 = dyn + Ab[oHd] * xa;
+              const double d2 = d1 + Ab[oH6] * xb;
+              dyn = hp ? (isv ? d1 : d2) : dyn;
+              lds_cd* ql = QLr + oQL;
+              const double bfv = beta * ri[0] - (((ql[0] * gm[0] + ql[2] * gm[2]) + ql[4] * gm[4]) +
+                                                 ((ql[1] * gm[1] + ql[3] * gm[3]) + ql[5] * gm[5]));
+              dyn = isv ? dyn + bfv : dyn;
               // friction rows: lane c < 3 owns row c, lane 3 rows 3 and 4 (all loads unconditional)
               const double q0 = qbc<0>(sf), q1 = qbc<1>(sf), q2 = qbc<2>(sf);
-              const int ta = cl ? c : 3;
-              const double frA = Ab[FO<N>(k, f, 2) + 5 + ta] * q2 +
-                                 Ab[FO<N>(k, f, ta >> 1) + 5 + (ta & 1)] * ((ta >> 1) == 0 ? q0 : q1);
-              const double frB = Ab[FO<N>(k, f, 2) + 9] * q2;
-              const double swg = Ab[fo + 4] * sf;
+              const double frA = Ab[oFb] * q2 + Ab[oFa] * (ta0 ? q0 : q1);
+              const double frB = Ab[oF4] * q2;
+              const double swg = Ab[oF + 4] * sf;
               ax[0] = cl ? dyn : frA;
               ax[1] = cl ? swg : frB;
               ax[2] = cl ? frA : 0.0;
@@ -1298,10 +1340,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
               const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
-              const double tt = zr + rinv_of(j) * y[j];
-              const double lj = lo_of(j), hj = hi_of(j);
-              const double zn = tt < lj ? lj : (tt > hj ? hj : tt);
-              y[j] = y[j] + rho_of(j) * (zr - zn);
+              const double tt = zr + ri[j] * y[j];
+              const double zn = tt < lo[j] ? lo[j] : (tt > hi[j] ? hi[j] : tt);
+              y[j] = y[j] + rr[j] * (zr - zn);
               z[j] = zn;
             }
             xf = p.alpha * sf + (1.0 - p.alpha) * xf;

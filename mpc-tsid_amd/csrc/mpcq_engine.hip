@@ -363,7 +363,6 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
   int cr = (t >> 4) & 1;            // sweep row (wave 0): 0 top-down, 1 bottom-up
   int rr_ = s < 12 ? s : 11;        // sweep lane's state index
   // store v at q when c holds, else into this lane's sink (branch-free)
-  auto st_if = [&](bool c_, double* q, double v) __attribute__((always_inline)) { *(c_ ? q : &sh.dump[t]) = v; };
   auto launder = [&]() __attribute__((always_inline)) {
     asm volatile("" : "+v"(Ab), "+v"(GHr), "+v"(SmR), "+v"(FWr), "+v"(QLr), "+v"(k), "+v"(f), "+v"(c), "+v"(cc), "+v"(ph), "+v"(fo), "+v"(xo),
                  "+v"(cr), "+v"(rr_));
@@ -573,10 +572,6 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       const unsigned cj = (cls >> (2 * j)) & 3u;
       return cj == RC_EQ ? r_eq : (cj == RC_INEQ ? r_in : kRhoMin);
     };
-    auto rinv_of = [&](int j) __attribute__((always_inline)) -> double {
-      const unsigned cj = (cls >> (2 * j)) & 3u;
-      return cj == RC_EQ ? ri_eq : (cj == RC_INEQ ? ri_in : 1.0 / kRhoMin);
-    };
     auto lo_of = [&](int j) __attribute__((always_inline)) -> double {
       if constexpr (FUSED) {
         if (j == 0) return cl ? bnd : -kInf * E[0];
@@ -619,32 +614,6 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       out[0] = cl ? dyn : fric_row(3, g0, g1, g2);
       out[1] = cl ? swg : fric_row(4, g0, g1, g2);
       out[2] = cl ? fric_row(c, g0, g1, g2) : 0.0;
-    };
-    // A' w for the own columns: wo = w of own rows, wbuf[k+1] = next stage's dynamics-row w
-    // force-column part of A' w (stage-local: DPP only)
-    auto colF_At = [&](const double (&wo)[3]) __attribute__((always_inline)) -> double {
-      const double w6 = rbc<LN(6)>(wo[0]), w7 = rbc<LN(7)>(wo[0]), w8 = rbc<LN(8)>(wo[0]);
-      const double w9 = rbc<LN(9)>(wo[0]), w10 = rbc<LN(10)>(wo[0]), w11 = rbc<LN(11)>(wo[0]);
-      const double wf0 = qbc<0>(wo[2]), wf1 = qbc<1>(wo[2]), wf2 = qbc<2>(wo[2]);
-      const double wf3 = qbc<3>(wo[0]), wf4 = qbc<3>(wo[1]);
-      double sA = Ab[fo] * sel3(cc, w6, w7, w8);
-      double sB = Ab[fo + 1] * w9;
-      sA += Ab[fo + 2] * w10;
-      sB += Ab[fo + 3] * w11;
-      sA += Ab[fo + 4] * wo[1];
-      sB += Ab[fo + 5] * (cc == 1 ? wf2 : wf0);
-      sA += Ab[fo + 6] * (cc == 1 ? wf3 : wf1);
-      const double e7 = Ab[fo + 7], e8 = Ab[fo + 8], e9 = Ab[fo + 9];  // friction rows 2..4 (cc == 2)
-      const double sC = cc == 2 ? (e7 * wf2 + e8 * wf3) + e9 * wf4 : 0.0;
-      return (sA + sB) + sC;
-    };
-    auto col_At = [&](const double (&wo)[3], const double (*wbuf)[12], double& of, double& oX) __attribute__((always_inline)) {
-      of = colF_At(wo);
-      const double* wn = wbuf[k < N - 1 ? k + 1 : k];
-      const double sX = Ab[xo] * wo[0];
-      const double x1 = sX + Ab[xo + 1] * wn[ph >= 6 ? ph - 6 : ph];
-      const double x2 = x1 + Ab[xo + 2] * wn[ph];
-      oX = k < N - 1 ? (ph >= 6 ? x2 : x1) : sX;
     };
     auto Pbf = [&]() __attribute__((always_inline)) { return cscale * (Df * P0f * Df); };
     auto PbX = [&]() __attribute__((always_inline)) { return cscale * (DX * P0X * DX); };
@@ -876,6 +845,47 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 
     // ---- residuals (OSQP update_info), uniform results ---------------------
     double pri_res = 0.0, dua_res = 0.0, eps_pri = 0.0, eps_dua = 0.0, s_pri = 0.0, s_dua = 0.0;
+  // per-lane constants of the ADMM loop and the residuals: LDS offsets, flags
+    const bool hp = k >= 1, isv = ph >= 6;
+    const int oXd = xo;                                                // Xd(k, ph)
+    const int oHd = XO<N>(hp ? k - 1 : 0, ph) + (ph < 6 ? 1 : 2);      // Hd(k, ph)
+    const int oH6 = XO<N>(hp ? k - 1 : 0, ph < 6 ? ph + 6 : 11) + 1;   // H6(k, ph)
+    const int oF = fo;
+    const int ta = cl ? c : 3;  // first own friction row
+    const bool ta0 = (ta >> 1) == 0;
+    const int oFa = FO<N>(k, f, ta >> 1) + 5 + (ta & 1), oFb = FO<N>(k, f, 2) + 5 + ta;
+    const int oF4 = FO<N>(k, f, 2) + 9;
+    const int oFW = 72 * k + 6 * ph, oFWc = 72 * k + (isv ? ph - 6 : 0);
+    const int oQL = 36 * k + 6 * (isv ? ph - 6 : 0);
+    const int oXS = 12 * (k + 1) + ph, oXSp = 12 * k + ph, oXSp6 = 12 * k + (ph < 6 ? ph + 6 : ph);
+    const double m2 = cc == 2 ? 1.0 : 0.0;
+    lds_cd* XSr = (lds_cd*)&sh.u.it.xs[0][0];
+    double* const Wbo = &sh.u.it.bo[k][ph];
+    double* const Wna = &sh.u.it.na[hp ? k - 1 : N - 1][ph];
+    double* const Wnb = &sh.u.it.nb[hp ? k - 1 : N - 1][hp ? (ph < 6 ? ph + 6 : ph - 6) : ph];
+    double* const Wdump = &sh.dump[t];
+    const int oB0 = FO<N>(k, 0, 0) + (ph >= 9 ? ph - 8 : 0);  // B row ph on force (fp, cp): + 24 fp + 7 cp
+    auto launder_p = [&]() __attribute__((always_inline)) {
+      asm volatile("" : "+v"(Ab), "+v"(GHr), "+v"(SmR), "+v"(FWr), "+v"(QLr), "+v"(XSr));
+    };
+    // force column of A' v for own-row values v (dynamics rows 6..11 by row broadcast,
+    // swing, friction by quad broadcast)
+    auto colF_off = [&](const double (&v)[3]) __attribute__((always_inline)) -> double {
+      const double w6 = rbc<LN(6)>(v[0]), w7 = rbc<LN(7)>(v[0]), w8 = rbc<LN(8)>(v[0]);
+      const double w9 = rbc<LN(9)>(v[0]), w10 = rbc<LN(10)>(v[0]), w11 = rbc<LN(11)>(v[0]);
+      const double wf0 = qbc<0>(v[2]), wf1 = qbc<1>(v[2]), wf2 = qbc<2>(v[2]);
+      const double wf3 = qbc<3>(v[0]), wf4 = qbc<3>(v[1]);
+      lds_cd* A = Ab + oF;
+      double sA = A[0] * (cc == 0 ? w6 : (cc == 1 ? w7 : w8));
+      double sB = A[1] * w9;
+      sA += A[2] * w10;
+      sB += A[3] * w11;
+      sA += A[4] * v[1];
+      sB += A[5] * (cc == 1 ? wf2 : wf0);
+      sA += A[6] * (cc == 1 ? wf3 : wf1);
+      const double sC = (A[7] * wf2 + A[8] * wf3) + A[9] * wf4;  // friction rows 2..4 (cc == 2)
+      return (sA + sB) + m2 * sC;
+    };
     // max over a 16-lane row: quad xor 1, xor 2, then rotations by 4 and 8
     auto row_max = [](double v) __attribute__((always_inline)) {
       v = fmax(v, dppd<0xB1>(v));
@@ -888,11 +898,34 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       sync_all();
       if (cl) { sh.u.it.xs[k + 1][ph] = xX; sh.u.it.bo[k][ph] = y[0]; }
       sync_all();
-      launder();
+      STAMP(4);
+      launder_p();
       double* const rowred = sh.red + 12 * k;  // this row's 12 partial maxima
       {  // primal side: A x - z on the own rows
         double ax[3], q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        row_A(xf, xX, ax);
+        {
+          double fall[12], bco[12];
+          gather12(xf, fall);
+#pragma unroll
+          for (int psi = 0; psi < 12; ++psi) {
+            const int fp = psi / 3, cp = psi % 3;
+            const double v = Ab[oB0 + 24 * fp + 7 * cp];
+            bco[psi] = (ph >= 9 || (isv && cp == ph - 6)) ? v : 0.0;
+          }
+          const double bfx = dot12(bco, fall);
+          double dyn = Ab[oXd] * xX;
+          const double d1 = dyn + Ab[oHd] * XSr[oXSp];
+          const double d2 = d1 + Ab[oH6] * XSr[oXSp6];
+          dyn = hp ? (isv ? d1 : d2) : dyn;
+          dyn = isv ? dyn + bfx : dyn;
+          const double q0 = qbc<0>(xf), q1 = qbc<1>(xf), q2 = qbc<2>(xf);
+          const double frA = Ab[oFb] * q2 + Ab[oFa] * (ta0 ? q0 : q1);
+          const double frB = Ab[oF4] * q2;
+          const double swg = Ab[oF + 4] * xf;
+          ax[0] = cl ? dyn : frA;
+          ax[1] = cl ? swg : frB;
+          ax[2] = cl ? frA : 0.0;
+        }
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           const double ei = 1.0 / E[j], d = ax[j] - z[j];
@@ -909,9 +942,18 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           if (s == 0) rowred[e] = v;
         }
       }
+      STAMP(5);
       {  // dual side: P x + A' y on the own columns
-        double atf, atX, q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        col_At(y, sh.u.it.bo, atf, atX);
+        double q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        const double atf = colF_off(y);
+        double atX;
+        {
+          const double* yn = sh.u.it.bo[k < N - 1 ? k + 1 : k];  // next stage's dynamics-row y
+          const double sXv = Ab[oXd] * y[0];
+          const double x1 = sXv + Ab[oXd + 1] * yn[isv ? ph - 6 : ph];
+          const double x2 = x1 + Ab[oXd + 2] * yn[ph];
+          atX = k < N - 1 ? (isv ? x2 : x1) : sXv;
+        }
         const double pxf = Pbf() * xf, pxX = PbX() * xX;
         const double dif = 1.0 / Df, diX = 1.0 / DX;
         const double df_ = pxf + atf, dX_ = pxX + atX;
@@ -930,6 +972,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         }
       }
       sync_all();
+      STAMP(8);
       // lane s of every row reduces quantity s % 12 over the N row partials, then
       // the row shares the 12 results by row_newbcast
       double qv[12];
@@ -1097,31 +1140,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       bool last_checked = false;
       int iter = 1;
       int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
-      // per-lane constants of the ADMM loop: LDS offsets, flags, scaled bounds
-      const bool hp = k >= 1, isv = ph >= 6;
-      const int oXd = xo;                                                // Xd(k, ph)
-      const int oHd = XO<N>(hp ? k - 1 : 0, ph) + (ph < 6 ? 1 : 2);      // Hd(k, ph)
-      const int oH6 = XO<N>(hp ? k - 1 : 0, ph < 6 ? ph + 6 : 11) + 1;   // H6(k, ph)
-      const int oF = fo;
-      const int ta = cl ? c : 3;  // first own friction row
-      const bool ta0 = (ta >> 1) == 0;
-      const int oFa = FO<N>(k, f, ta >> 1) + 5 + (ta & 1), oFb = FO<N>(k, f, 2) + 5 + ta;
-      const int oF4 = FO<N>(k, f, 2) + 9;
-      const int oFW = 72 * k + 6 * ph, oFWc = 72 * k + (isv ? ph - 6 : 0);
-      const int oQL = 36 * k + 6 * (isv ? ph - 6 : 0);
-      const int oXS = 12 * (k + 1) + ph, oXSp = 12 * k + ph, oXSp6 = 12 * k + (ph < 6 ? ph + 6 : ph);
-      const double m2 = cc == 2 ? 1.0 : 0.0;
-      lds_cd* XSr = (lds_cd*)&sh.u.it.xs[0][0];
-      double* const Wbo = &sh.u.it.bo[k][ph];
-      double* const Wna = &sh.u.it.na[hp ? k - 1 : N - 1][ph];
-      double* const Wnb = &sh.u.it.nb[hp ? k - 1 : N - 1][hp ? (ph < 6 ? ph + 6 : ph - 6) : ph];
-      double* const Wdump = &sh.dump[t];
       double lo[3], hi[3];
 #pragma unroll
       for (int j = 0; j < 3; ++j) { lo[j] = lo_of(j); hi[j] = hi_of(j); }
-      auto launder_p = [&]() __attribute__((always_inline)) {
-        asm volatile("" : "+v"(Ab), "+v"(GHr), "+v"(SmR), "+v"(FWr), "+v"(QLr), "+v"(XSr));
-      };
       for (;;) {
         if (!factor(p.sigma)) { status = MPCQ_STATUS_FACTOR_FAILED; break; }
         STAMP(2);
@@ -1135,23 +1156,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           double w[3];
 #pragma unroll
           for (int j = 0; j < 3; ++j) w[j] = rr[j] * z[j] - y[j];
-          double bf;
-          {  // force column of A' w: dynamics rows 6..11 (row broadcast), swing, friction (quad)
-            const double w6 = rbc<LN(6)>(w[0]), w7 = rbc<LN(7)>(w[0]), w8 = rbc<LN(8)>(w[0]);
-            const double w9 = rbc<LN(9)>(w[0]), w10 = rbc<LN(10)>(w[0]), w11 = rbc<LN(11)>(w[0]);
-            const double wf0 = qbc<0>(w[2]), wf1 = qbc<1>(w[2]), wf2 = qbc<2>(w[2]);
-            const double wf3 = qbc<3>(w[0]), wf4 = qbc<3>(w[1]);
-            lds_cd* A = Ab + oF;
-            double sA = A[0] * (cc == 0 ? w6 : (cc == 1 ? w7 : w8));
-            double sB = A[1] * w9;
-            sA += A[2] * w10;
-            sB += A[3] * w11;
-            sA += A[4] * w[1];
-            sB += A[5] * (cc == 1 ? wf2 : wf0);
-            sA += A[6] * (cc == 1 ? wf3 : wf1);
-            const double sC = (A[7] * wf2 + A[8] * wf3) + A[9] * wf4;  // friction rows 2..4 (cc == 2)
-            bf = ((sA + sB) + m2 * sC) + p.sigma * xf;                 // - q, q = 0
-          }
+          const double bf = colF_off(w) + p.sigma * xf;  // b_f = sigma x_f + A_f' w (- q, q = 0)
           // u = F b_f (kept for the forces) and beta = R B u = (F W)' b_f (rows 6..11)
           double beta, uf;
           {
@@ -1175,8 +1180,6 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           }
           sync_all();
           STAMP(3);
-          STAMP(4);
-          STAMP(5);
           // P5-P7: the state solve on wave 0 alone (no block barrier inside).  Rows
           // 0 / 2 run the top-down sweep (columns 0-5 / 6-11 of each step's
           // matrix), rows 1 / 3 the bottom-up one; the two halves of every product
@@ -1298,7 +1301,6 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           }
           sync_all();
           STAMP(7);
-          STAMP(8);
           // P8: forces f_k = F_k (b_f - R B' g) = u - (F W) g, with g = Xd X_{k+1} + Hd X_k
           // on the velocity rows (the states' part of those rows)
           double sf, sX, gm[6];

@@ -13,8 +13,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "mpc-tsid_amd"))
 os.environ.setdefault("MPCQ_LIB_VARIANT", "stamps")
 
-NAMES = ["prologue", "scaling", "factor", "iter:w,b,u,beta,bt", "-", "-", "iter:inward sweeps+S^-1 y",
-         "iter:outward sweeps", "-", "iter:forces", "iter:z/y/x update", "iter:check+adapt", "epilogue", "fac:phaseP", "fac:phaseS"]
+NAMES = ["prologue", "scaling", "factor", "iter:w,b,u,beta,bt", "chk:publish", "chk:primal", "iter:inward sweeps+S^-1 y",
+         "iter:outward sweeps", "chk:dual", "iter:forces", "iter:z/y/x update", "chk:reduce+adapt", "epilogue", "fac:phaseP", "fac:phaseS"]
 
 
 def main():

@@ -99,6 +99,23 @@ __device__ __forceinline__ double rbc(double v) { return dppd<0x150 + J>(v); }
 template <int J>
 __device__ __forceinline__ double qbc(double v) { return dppd<85 * J>(v); }
 
+// i0 + sum_{j<6} g_j * v_j with v_j broadcast from lane j of the row, the broadcasts
+// folded into v_fmac_f64_dpp (row_newbcast is the one DPP64 control); two chains.
+// s_nop 1: a VALU write of v followed by a DPP read of it needs two wait states.
+__device__ __forceinline__ double bdot6(const double (&g)[6], double v, double i0) {
+  double a0 = i0, a1 = 0.0;
+  asm("s_nop 1\n\t"
+      "v_fmac_f64_dpp %0, %2, %3 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %4 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %5 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %6 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %7 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %8 row_newbcast:5 row_mask:0xf bank_mask:0xf"
+      : "+v"(a0), "+v"(a1)
+      : "v"(v), "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]), "v"(g[4]), "v"(g[5]));
+  return a0 + a1;
+}
+
 template <int... J>
 __device__ __forceinline__ void gather_seq(double v, double (&all)[12], std::integer_sequence<int, J...>) {
   ((all[J] = rbc<LN(J)>(v)), ...);
@@ -624,37 +641,34 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     auto Qv = [&](int kk, int j1, int j2) __attribute__((always_inline)) { return GHr[144 * kk + 6 * j1 + j2]; };
     // The factorisation's row builders are branch-free: every load is unconditional
     // (indices clamped in range) and the structure is applied by selects.
+    // The couplings are sparse: row i of L_kk (and column i) has its nonzeros on
+    // column a(i) = i mod 6 and the velocity columns 6..11, so a row is kept as
+    // (ca, c6[0..5]).
     // Row i of L_kk (kk >= 1): the dynamics rows of stage kk on (X_{kk+1}[i], X_kk[ci]).
-    auto Ctop = [&](int kk, int i, double (&Cr)[12]) __attribute__((always_inline)) {
+    auto Ctop = [&](int kk, int i, double& ca, double (&c6)[6]) __attribute__((always_inline)) {
       const int iq = i >= 6 ? i - 6 : 0;
       const double ri = rdy(kk, i), xi = Xd(kk, i), hi = Hd(kk, i), h6 = H6(kk, i < 6 ? i : 0);
       const double dv = ri * xi * hi, tv = ri * xi * h6;
+      ca = i < 6 ? dv : 0.0;
 #pragma unroll
-      for (int ci = 0; ci < 12; ++ci) {
-        double v = (ci == i) ? dv : 0.0;
-        v = (i < 6 && ci == i + 6) ? tv : v;
-        if (ci >= 6) {
-          const double sc = xi * Qv(kk, iq, ci - 6) * Hd(kk, ci);
-          v = i >= 6 ? v - sc : v;
-        }
-        Cr[ci] = v;
+      for (int j = 0; j < 6; ++j) {
+        const double sc = xi * Qv(kk, iq, j) * Hd(kk, 6 + j);
+        const double vv = (6 + j == i ? dv : 0.0) - sc;
+        c6[j] = i < 6 ? (j == i ? tv : 0.0) : vv;
       }
     };
     // Column i of L_kk (kk >= 1), i.e. row i of L_kk'.
-    auto Cbot = [&](int kk, int i, double (&Cr)[12]) __attribute__((always_inline)) {
+    auto Cbot = [&](int kk, int i, double& ca, double (&c6)[6]) __attribute__((always_inline)) {
       const int ip = i >= 6 ? i - 6 : 0;
       const double hi = Hd(kk, i);
       const double dv = rdy(kk, i) * Xd(kk, i) * hi;
       const double tv = rdy(kk, ip) * Xd(kk, ip) * H6(kk, ip);
+      ca = i < 6 ? dv : tv;
 #pragma unroll
-      for (int jr = 0; jr < 12; ++jr) {
-        double v = (jr == i) ? dv : 0.0;
-        v = (i >= 6 && jr == i - 6) ? tv : v;
-        if (jr >= 6) {
-          const double sc = Xd(kk, jr) * Qv(kk, jr - 6, ip) * hi;
-          v = i >= 6 ? v - sc : v;
-        }
-        Cr[jr] = v;
+      for (int j = 0; j < 6; ++j) {
+        const double sc = Xd(kk, 6 + j) * Qv(kk, j, ip) * hi;
+        const double vv = (6 + j == i ? dv : 0.0) - sc;
+        c6[j] = i >= 6 ? vv : 0.0;
       }
     };
     // Row i of D_kk (the state block of X_{kk+1}).
@@ -771,23 +785,26 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       // (Sb), giving H_k -> GH[k+1].  Ro -= (C S^{-1}) C'.  Products run block by
       // block (a compiler fence per block keeps the loads from piling up).
       auto couple = [&](bool upper, double (&Ro)[12]) __attribute__((always_inline)) {
-        double Cr[12];
-        if (upper) Ctop(k, ph, Cr);
-        else Cbot(k + 1, ph, Cr);
-        double* const Cb = upper ? Lt : Lb;
+        double ca, c6[6];
+        if (upper) Ctop(k, ph, ca, c6);
+        else Cbot(k + 1, ph, ca, c6);
+        double* const Cb = upper ? Lt : Lb;  // compact rows: 7 per row
         const double* const Sp = upper ? St : Sb;
         if (cl) {
+          Cb[7 * ph] = ca;
 #pragma unroll
-          for (int ci = 0; ci < 12; ++ci) Cb[12 * ph + ci] = Cr[ci];
+          for (int j = 0; j < 6; ++j) Cb[7 * ph + 1 + j] = c6[j];
         }
         wave_sync();  // C rows visible (and this row's reads of GH[k], GH[k+1] are done)
+        const int ar = ph < 6 ? ph : ph - 6;
         double G[12];
 #pragma unroll
-        for (int ci = 0; ci < 12; ++ci) G[ci] = 0.0;
+        for (int ci = 0; ci < 12; ++ci) G[ci] = ca * Sp[12 * ar + ci];
+        asm volatile("" ::: "memory");
 #pragma unroll
-        for (int jj = 0; jj < 12; ++jj) {
+        for (int j = 0; j < 6; ++j) {
 #pragma unroll
-          for (int ci = 0; ci < 12; ++ci) G[ci] = fma(Cr[jj], Sp[12 * jj + ci], G[ci]);
+          for (int ci = 0; ci < 12; ++ci) G[ci] = fma(c6[j], Sp[12 * (6 + j) + ci], G[ci]);
           asm volatile("" ::: "memory");
         }
         if (cl) {
@@ -797,12 +814,13 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         }
 #pragma unroll
         for (int ci = 0; ci < 12; ++ci) {
-          double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-          for (int jj = 0; jj < 12; jj += 2) {
-            a0 = fma(G[jj], Cb[12 * ci + jj], a0);
-            a1 = fma(G[jj + 1], Cb[12 * ci + jj + 1], a1);
-          }
+          const double* const cr = Cb + 7 * ci;
+          double a0 = G[ci < 6 ? ci : ci - 6] * cr[0], a1 = G[6] * cr[1];
+          a0 = fma(G[7], cr[2], a0);
+          a1 = fma(G[8], cr[3], a1);
+          a0 = fma(G[9], cr[4], a0);
+          a1 = fma(G[10], cr[5], a1);
+          a0 = fma(G[11], cr[6], a0);
           Ro[ci] -= a0 + a1;
           asm volatile("" ::: "memory");
         }
@@ -1185,67 +1203,62 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           // matrix), rows 1 / 3 the bottom-up one; the two halves of every product
           // combine by permlane32_swap.  Inward, each step also forms
           // w_k = S_k^{-1} y_k of the stage the previous step finished (off the
-          // dependency chain, sharing its broadcasts); then the meeting stage and
+          // dependency chain, sharing its broadcast); then the meeting stage and
           // the outward sweeps.
           const int half = (t >> 5) & 1, hoff = 6 * half;
+          auto bt_at = [&](lds_cd* q) __attribute__((always_inline)) {
+            return (q[0] + q[12 * N]) + q[24 * N];
+          };
+          double xp = 0.0;
           if (t < 64) {
             // Inward step j: top kk = j (G_kk in GH[kk]), bottom kk = N-1-j (H_kk in
             // GH[kk+1]).  Pointers walk the stages (+-1 slot per step); the asm keeps
             // them in registers so each step's loads stay in that step.
             const int gs = cr == 0 ? 144 : -144, bs = cr == 0 ? 12 : -12;
             lds_cd* GpN = GHr + 144 * (cr == 0 ? 1 : N - 1) + 12 * rr_ + hoff;  // G / H of step 1
-            lds_cd* SpN = SmR + 144 * (cr == 0 ? 0 : N - 1) + 12 * rr_ + hoff;  // S^{-1} of stage kk(0)
             lds_cd* BpN = (lds_cd*)&sh.u.it.bo[cr == 0 ? 0 : N - 1][rr_];        // bo; na, nb at +12N, +24N
+            lds_cd* SpN = SmR + 144 * (cr == 0 ? 0 : N - 1) + 12 * rr_ + hoff;  // S^{-1} of stage kk(0)
             lds_d* Yp = (lds_d*)&sh.u.it.yv[cr == 0 ? 0 : N - 1][rr_];
-            auto bt_at = [&](lds_cd* q) __attribute__((always_inline)) {
-              return (q[0] + q[12 * N]) + q[24 * N];
-            };
             double yp = bt_at(BpN);
             BpN += bs;
-            double g[6], sv[6], bq;
+            // the next step's rhs parts stay raw until that step (no LDS wait inside this one)
+            double g[6], sv[6], b0 = BpN[0], b1 = BpN[12 * N], b2 = BpN[24 * N];
 #pragma unroll
             for (int i = 0; i < 6; ++i) { g[i] = GpN[i]; sv[i] = SpN[i]; }
             GpN += gs;
             SpN += gs;
-            bq = bt_at(BpN);
             BpN += bs;
 #pragma unroll
             for (int j = 1; j <= MID; ++j) {
-              asm volatile("" : "+v"(GpN), "+v"(SpN), "+v"(BpN), "+v"(Yp));
+              asm volatile("" : "+v"(GpN), "+v"(SpN), "+v"(BpN), "+v"(Yp) : : "memory");
               double gc[6], sc[6];
 #pragma unroll
               for (int i = 0; i < 6; ++i) { gc[i] = g[i]; sc[i] = sv[i]; }
-              const double bc = bq;
+              asm volatile("" : "+v"(b0), "+v"(b1), "+v"(b2));
+              const double bc = (b0 + b1) + b2;
               if (j < MID) {  // prefetch the next step's half rows and right-hand side
 #pragma unroll
                 for (int i = 0; i < 6; ++i) { g[i] = GpN[i]; sv[i] = SpN[i]; }
                 GpN += gs;
                 SpN += gs;
-                bq = bt_at(BpN);
+                b0 = BpN[0]; b1 = BpN[12 * N]; b2 = BpN[24 * N];
                 BpN += bs;
               }
-              double yb[6];
-              {
-                const double ys = half_shift(yp);
-                yb[0] = rbc<0>(ys); yb[1] = rbc<1>(ys); yb[2] = rbc<2>(ys);
-                yb[3] = rbc<3>(ys); yb[4] = rbc<4>(ys); yb[5] = rbc<5>(ys);
-              }
+              asm volatile("" : : : "memory");  // the prefetch is issued here, not sunk to its use
               // y = b - G y_prev with -G stored: half 0 starts its chains from b
               const double i0 = half == 0 ? bc : 0.0;
-              const double acc = pair_sum((fma(gc[4], yb[4], fma(gc[2], yb[2], fma(gc[0], yb[0], i0)))) +
-                                          (fma(gc[5], yb[5], fma(gc[3], yb[3], gc[1] * yb[1]))));
+              const double ys = half_shift(yp);
+              const double acc = pair_sum(bdot6(gc, ys, i0));
               // off the chain: w of the stage the previous step finished (kk(j-1))
-              const double wv = pair_sum(((sc[0] * yb[0] + sc[2] * yb[2]) + sc[4] * yb[4]) +
-                                         ((sc[1] * yb[1] + sc[3] * yb[3]) + sc[5] * yb[5]));
+              const double wv = pair_sum(bdot6(sc, ys, 0.0));
               const bool wok = (cr == 0 || j == 1 || N - j >= MID) && (cr == 0 ? j - 1 : N - j) != MID;
               *(wok && half == 0 && s < 12 ? Yp : (lds_d*)&sh.dump[t]) = wv;
               Yp += bs;
               yp = (cr == 0 || N - 1 - j >= MID) ? acc : yp;
             }
-            // meeting stage: x_m = M^{-1} (y_m + v_m - b_m)
             if (half == 0) sh.red[RMID + 16 * cr + s] = yp;
             wave_sync();
-            double xp;
+            // meeting stage: x_m = M^{-1} (y_m + v_m - b_m)
             {
               const double cm = sh.red[RMID + rr_] + sh.red[RMID + 16 + rr_] -
                                 bt_at((lds_cd*)&sh.u.it.bo[MID][rr_]);
@@ -1264,6 +1277,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             lds_cd* MpN = GHr + 144 * (cr == 0 ? MID : MID + 1) + rr_ + 12 * hoff;
             lds_cd* WpN = (lds_cd*)&sh.u.it.yv[cr == 0 ? MID - 1 : MID + 1][rr_];
             lds_d* Xp = (lds_d*)&sh.u.it.xs[cr == 0 ? MID : MID + 2][rr_];
+            double bq;
 #pragma unroll
             for (int i = 0; i < 6; ++i) g[i] = MpN[12 * i];
             MpN += ms;
@@ -1272,7 +1286,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             WpN += ws;
 #pragma unroll
             for (int j = 1; j <= MID; ++j) {
-              asm volatile("" : "+v"(MpN), "+v"(WpN), "+v"(Xp));
+              asm volatile("" : "+v"(MpN), "+v"(WpN), "+v"(Xp) : : "memory");
               double gc[6];
 #pragma unroll
               for (int i = 0; i < 6; ++i) gc[i] = g[i];
@@ -1284,15 +1298,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
                 bq = WpN[0];
                 WpN += ws;
               }
-              double xb[6];
-              {
-                const double xs_ = half_shift(xp);
-                xb[0] = rbc<0>(xs_); xb[1] = rbc<1>(xs_); xb[2] = rbc<2>(xs_);
-                xb[3] = rbc<3>(xs_); xb[4] = rbc<4>(xs_); xb[5] = rbc<5>(xs_);
-              }
+              asm volatile("" : : : "memory");
               const double i0 = half == 0 ? bc : 0.0;  // x = w - G' x_next with -G stored
-              const double acc = pair_sum((fma(gc[4], xb[4], fma(gc[2], xb[2], fma(gc[0], xb[0], i0)))) +
-                                          (fma(gc[5], xb[5], fma(gc[3], xb[3], gc[1] * xb[1]))));
+              const double acc = pair_sum(bdot6(gc, half_shift(xp), i0));
               const bool act = cr == 0 || MID + j <= N - 1;
               xp = act ? acc : xp;
               *(act && half == 0 && s < 12 ? Xp : (lds_d*)&sh.dump[t]) = acc;

@@ -1221,7 +1221,10 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             lds_d* Yp = (lds_d*)&sh.u.it.yv[cr == 0 ? 0 : N - 1][rr_];
             double yp = bt_at(BpN);
             BpN += bs;
-            // the next step's rhs parts stay raw until that step (no LDS wait inside this one)
+            // right-hand sides run two steps ahead: step j sums the one of step j+1
+            // (loaded during step j-1) and loads the one of step j+2
+            double bcn = bt_at(BpN);
+            BpN += bs;
             double g[6], sv[6], b0 = BpN[0], b1 = BpN[12 * N], b2 = BpN[24 * N];
 #pragma unroll
             for (int i = 0; i < 6; ++i) { g[i] = GpN[i]; sv[i] = SpN[i]; }
@@ -1234,21 +1237,23 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               double gc[6], sc[6];
 #pragma unroll
               for (int i = 0; i < 6; ++i) { gc[i] = g[i]; sc[i] = sv[i]; }
-              asm volatile("" : "+v"(b0), "+v"(b1), "+v"(b2));
-              const double bc = (b0 + b1) + b2;
-              if (j < MID) {  // prefetch the next step's half rows and right-hand side
+              const double bc = bcn;
+              if (j < MID) {  // prefetch the next step's half rows
 #pragma unroll
                 for (int i = 0; i < 6; ++i) { g[i] = GpN[i]; sv[i] = SpN[i]; }
                 GpN += gs;
                 SpN += gs;
-                b0 = BpN[0]; b1 = BpN[12 * N]; b2 = BpN[24 * N];
-                BpN += bs;
               }
               asm volatile("" : : : "memory");  // the prefetch is issued here, not sunk to its use
               // y = b - G y_prev with -G stored: half 0 starts its chains from b
               const double i0 = half == 0 ? bc : 0.0;
               const double ys = half_shift(yp);
               const double acc = pair_sum(bdot6(gc, ys, i0));
+              if (j < MID) bcn = (b0 + b1) + b2;
+              if (j + 2 <= MID) {
+                b0 = BpN[0]; b1 = BpN[12 * N]; b2 = BpN[24 * N];
+                BpN += bs;
+              }
               // off the chain: w of the stage the previous step finished (kk(j-1))
               const double wv = pair_sum(bdot6(sc, ys, 0.0));
               const bool wok = (cr == 0 || j == 1 || N - j >= MID) && (cr == 0 ? j - 1 : N - j) != MID;

@@ -104,7 +104,8 @@ __device__ __forceinline__ double qbc(double v) { return dppd<85 * J>(v); }
 // s_nop 1: a VALU write of v followed by a DPP read of it needs two wait states.
 __device__ __forceinline__ double bdot6(const double (&g)[6], double v, double i0) {
   double a0 = i0, a1 = 0.0;
-  asm("s_nop 1\n\t"
+  // volatile: stays after the sweeps' prefetch fences, so the loads issue first
+  asm volatile("s_nop 1\n\t"
       "v_fmac_f64_dpp %0, %2, %3 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
       "v_fmac_f64_dpp %1, %2, %4 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
       "v_fmac_f64_dpp %0, %2, %5 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
@@ -1248,14 +1249,17 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               // y = b - G y_prev with -G stored: half 0 starts its chains from b
               const double i0 = half == 0 ? bc : 0.0;
               const double ys = half_shift(yp);
-              const double acc = pair_sum(bdot6(gc, ys, i0));
+              // the chain's products, then (off the chain) w of the stage the previous
+              // step finished (kk(j-1)), issued into the chain's latency
+              const double pa = bdot6(gc, ys, i0);
+              const double pw = bdot6(sc, ys, 0.0);
+              const double acc = pair_sum(pa);
               if (j < MID) bcn = (b0 + b1) + b2;
               if (j + 2 <= MID) {
                 b0 = BpN[0]; b1 = BpN[12 * N]; b2 = BpN[24 * N];
                 BpN += bs;
               }
-              // off the chain: w of the stage the previous step finished (kk(j-1))
-              const double wv = pair_sum(bdot6(sc, ys, 0.0));
+              const double wv = pair_sum(pw);
               const bool wok = (cr == 0 || j == 1 || N - j >= MID) && (cr == 0 ? j - 1 : N - j) != MID;
               *(wok && half == 0 && s < 12 ? Yp : (lds_d*)&sh.dump[t]) = wv;
               Yp += bs;

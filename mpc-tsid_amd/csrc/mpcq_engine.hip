@@ -171,6 +171,15 @@ __device__ __forceinline__ double half_shift(double v) {
   const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), 0x12A, 0xC, 0xF, false);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+// v(lane l) + v(lane l +- 16): rows 0 + 1 and rows 2 + 3, the same sum order in both rows
+__device__ __forceinline__ double row_pair_sum(double v) {
+  const long long b = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  const double a0 = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
+  const double a1 = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+  return a0 + a1;
+}
 // v(lane l) + v(lane l +- 32): rows 0 + 2 and rows 1 + 3, the same sum order in both halves
 __device__ __forceinline__ double pair_sum(double v) {
   const long long b = __double_as_longlong(v);
@@ -338,7 +347,7 @@ struct Smem {
       double St[144], Sb[144], Lt[144], Lb[144];  // sweep hand-offs of the factorisation
     } fa;
   } u;
-  double red[12 * N + 32];  // per-row partial reductions [12 N); [12 N, +32) sweep meeting point
+  double red[12 * N];  // per-row partial reductions
   double dump[16 * N];      // per-lane sink: predicated stores write here instead of branching
   int flag[4];
 };
@@ -358,7 +367,6 @@ struct Prologue {
 template <int N, bool FUSED, bool SOLVE>
 __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, LaunchArgs a) {
   constexpr int NW = N / 4, T = 16 * N, n = 24 * N, m = 44 * N, nnz = 126 * N - 18, MID = N / 2;
-  constexpr int RMID = 12 * N;  // sweep meeting point inside red[]
   __shared__ Smem<N> sh;
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
   // lane coordinates; the loops launder them (see launder()) so that the
@@ -1244,6 +1252,11 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
                 for (int i = 0; i < 6; ++i) { g[i] = GpN[i]; sv[i] = SpN[i]; }
                 GpN += gs;
                 SpN += gs;
+              } else {  // last step: the meeting stage's M^{-1} half row and right-hand side
+#pragma unroll
+                for (int i = 0; i < 6; ++i) g[i] = GHr[12 * rr_ + hoff + i];
+                lds_cd* q = (lds_cd*)&sh.u.it.bo[MID][rr_];
+                b0 = q[0]; b1 = q[12 * N]; b2 = q[24 * N];
               }
               asm volatile("" : : : "memory");  // the prefetch is issued here, not sunk to its use
               // y = b - G y_prev with -G stored: half 0 starts its chains from b
@@ -1265,16 +1278,11 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               Yp += bs;
               yp = (cr == 0 || N - 1 - j >= MID) ? acc : yp;
             }
-            if (half == 0) sh.red[RMID + 16 * cr + s] = yp;
-            wave_sync();
-            // meeting stage: x_m = M^{-1} (y_m + v_m - b_m)
+            // meeting stage: x_m = M^{-1} (y_m + v_m - b_m); the top (row 0 / 2) and
+            // bottom (row 1 / 3) results meet by permlane16_swap
             {
-              const double cm = sh.red[RMID + rr_] + sh.red[RMID + 16 + rr_] -
-                                bt_at((lds_cd*)&sh.u.it.bo[MID][rr_]);
-              double gm[6];
-#pragma unroll
-              for (int i = 0; i < 6; ++i) gm[i] = GHr[12 * rr_ + hoff + i];
-              xp = pair_sum(dot6(gm, half_shift(cm)));
+              const double cm = row_pair_sum(yp) - ((b0 + b1) + b2);
+              xp = pair_sum(bdot6(g, half_shift(cm), 0.0));
               if (cr == 0 && half == 0 && s < 12) sh.u.it.xs[MID + 1][rr_] = xp;
             }
             STAMP(6);

@@ -210,6 +210,15 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 // a wave-uniform double kept in SGPRs
+// Launder an LDS base pointer: the pointer round-trips a VGPR through an empty asm
+// (opaque to the optimiser, so loads through it are not hoisted out of loops)
+// and comes back uniform in an SGPR via readfirstlane, costing no VGPR.
+template <typename P>
+__device__ __forceinline__ void lds_uniform(P*& q) {
+  asm volatile("" : "+v"(q));
+  q = reinterpret_cast<P*>(static_cast<unsigned long>(
+      __builtin_amdgcn_readfirstlane(static_cast<int>(reinterpret_cast<unsigned long>(q)))));
+}
 __device__ __forceinline__ double uni(double v) {
   const long long bits = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readfirstlane((int)bits);
@@ -390,7 +399,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
   int rr_ = s < 12 ? s : 11;        // sweep lane's state index
   // store v at q when c holds, else into this lane's sink (branch-free)
   auto launder = [&]() __attribute__((always_inline)) {
-    asm volatile("" : "+v"(Ab), "+v"(GHr), "+v"(SmR), "+v"(FWr), "+v"(QLr), "+v"(k), "+v"(f), "+v"(c), "+v"(cc), "+v"(ph), "+v"(fo), "+v"(xo),
+    lds_uniform(Ab); lds_uniform(GHr); lds_uniform(SmR); lds_uniform(FWr); lds_uniform(QLr);
+    asm volatile("" : "+v"(k), "+v"(f), "+v"(c), "+v"(cc), "+v"(ph), "+v"(fo), "+v"(xo),
                  "+v"(cr), "+v"(rr_));
   };
   (void)lane;
@@ -893,7 +903,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     double* const Wdump = &sh.dump[t];
     const int oB0 = FO<N>(k, 0, 0) + (ph >= 9 ? ph - 8 : 0);  // B row ph on force (fp, cp): + 24 fp + 7 cp
     auto launder_p = [&]() __attribute__((always_inline)) {
-      asm volatile("" : "+v"(Ab), "+v"(GHr), "+v"(SmR), "+v"(FWr), "+v"(QLr), "+v"(XSr));
+      lds_uniform(Ab); lds_uniform(GHr); lds_uniform(SmR); lds_uniform(FWr); lds_uniform(QLr); lds_uniform(XSr);
     };
     // force column of A' v for own-row values v (dynamics rows 6..11 by row broadcast,
     // swing, friction by quad broadcast)

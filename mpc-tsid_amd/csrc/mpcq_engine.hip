@@ -180,6 +180,20 @@ __device__ __forceinline__ double row_pair_sum(double v) {
   const double a1 = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
   return a0 + a1;
 }
+__device__ __forceinline__ double row_pair_max(double v) {
+  const long long b = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  return fmax(__longlong_as_double(((long long)hi[0] << 32) | lo[0]),
+              __longlong_as_double(((long long)hi[1] << 32) | lo[1]));
+}
+__device__ __forceinline__ double pair_max(double v) {
+  const long long b = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  return fmax(__longlong_as_double(((long long)hi[0] << 32) | lo[0]),
+              __longlong_as_double(((long long)hi[1] << 32) | lo[1]));
+}
 // v(lane l) + v(lane l +- 32): rows 0 + 2 and rows 1 + 3, the same sum order in both halves
 __device__ __forceinline__ double pair_sum(double v) {
   const long long b = __double_as_longlong(v);
@@ -931,13 +945,17 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       v = fmax(v, dppd<0x128>(v));
       return v;
     };
+    // The states and dynamics-row duals are published in yv / bo, which the sweeps
+    // no longer need (xs still feeds the force recovery of slower waves); lane s
+    // of each row then owns residual quantity s, reduced over the wave's rows by
+    // permlane swaps and over the waves through red[].
     auto update_info = [&]() __attribute__((always_inline)) {
-      sync_all();
-      if (cl) { sh.u.it.xs[k + 1][ph] = xX; sh.u.it.bo[k][ph] = y[0]; }
+      if (cl) { sh.u.it.yv[k][ph] = xX; sh.u.it.bo[k][ph] = y[0]; }
       sync_all();
       STAMP(4);
       launder_p();
-      double* const rowred = sh.red + 12 * k;  // this row's 12 partial maxima
+      lds_cd* const YV = (lds_cd*)&sh.u.it.yv[0][0];  // X_{k'} of stage k' >= 1 at 12 (k' - 1)
+      double mine = 0.0;                              // this lane's row maximum (quantity s)
       {  // primal side: A x - z on the own rows
         double ax[3], q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         {
@@ -951,8 +969,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           }
           const double bfx = dot12(bco, fall);
           double dyn = Ab[oXd] * xX;
-          const double d1 = dyn + Ab[oHd] * XSr[oXSp];
-          const double d2 = d1 + Ab[oH6] * XSr[oXSp6];
+          const double d1 = dyn + Ab[oHd] * YV[oXSp - 12];
+          const double d2 = d1 + Ab[oH6] * YV[oXSp6 - 12];
           dyn = hp ? (isv ? d1 : d2) : dyn;
           dyn = isv ? dyn + bfx : dyn;
           const double q0 = qbc<0>(xf), q1 = qbc<1>(xf), q2 = qbc<2>(xf);
@@ -976,7 +994,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma unroll
         for (int e = 0; e < 6; ++e) {
           const double v = row_max(q6[e]);
-          if (s == 0) rowred[e] = v;
+          mine = s == e ? v : mine;
         }
       }
       STAMP(5);
@@ -1005,19 +1023,19 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma unroll
         for (int e = 0; e < 6; ++e) {
           const double v = row_max(q6[e]);
-          if (s == 0) rowred[6 + e] = v;
+          mine = s == 6 + e ? v : mine;
         }
       }
+      mine = pair_max(row_pair_max(mine));  // the wave's four rows
+      if (lane < 12) sh.red[12 * wv + lane] = mine;
       sync_all();
       STAMP(8);
-      // lane s of every row reduces quantity s % 12 over the N row partials, then
-      // the row shares the 12 results by row_newbcast
       double qv[12];
       {
-        const int e = s < 12 ? s : s - 12;
-        double v = 0.0;
-#pragma nounroll
-        for (int r = 0; r < N; ++r) v = fmax(v, sh.red[12 * r + e]);
+        const int e = s < 12 ? s : 0;
+        double v = sh.red[e];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) v = fmax(v, sh.red[12 * w + e]);
         gather_direct12(v, qv);
       }
       const double cinv = 1.0 / cscale;
@@ -1027,6 +1045,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       eps_dua = p.eps_abs + p.eps_rel * cinv * fmax(qv[7], qv[8]);
       s_pri = qv[3] / (fmax(qv[4], qv[5]) + kDivTol);
       s_dua = qv[9] / (fmax(qv[10], qv[11]) + kDivTol);
+      // uniform by construction; readfirstlane lets the compiler see it
+      pri_res = uni(pri_res); dua_res = uni(dua_res); eps_pri = uni(eps_pri);
+      eps_dua = uni(eps_dua); s_pri = uni(s_pri); s_dua = uni(s_dua);
       sync_all();
     };
     auto converged = [&](double fac) __attribute__((always_inline)) {

@@ -99,6 +99,29 @@ __device__ __forceinline__ double rbc(double v) { return dppd<0x150 + J>(v); }
 template <int J>
 __device__ __forceinline__ double qbc(double v) { return dppd<85 * J>(v); }
 
+// i0 + sum_{j<12} g_j * v_j, v_j broadcast from lane j of the row (v_fmac_f64_dpp);
+// two interleaved chains.  s_nop 1: a VALU write of v then a DPP read of it needs two
+// wait states.
+__device__ __forceinline__ double bdot12(const double (&g)[12], double v, double i0) {
+  double a0 = i0, a1 = 0.0;
+  asm volatile("s_nop 1\n\t"
+      "v_fmac_f64_dpp %0, %2, %3 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %4 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %5 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %6 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %7 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %8 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %9 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %10 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %14 row_newbcast:11 row_mask:0xf bank_mask:0xf"
+      : "+v"(a0), "+v"(a1)
+      : "v"(v), "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]), "v"(g[4]), "v"(g[5]), "v"(g[6]), "v"(g[7]),
+        "v"(g[8]), "v"(g[9]), "v"(g[10]), "v"(g[11]));
+  return a0 + a1;
+}
 // i0 + sum_{j<6} g_j * v_j with v_j broadcast from lane j of the row, the broadcasts
 // folded into v_fmac_f64_dpp (row_newbcast is the one DPP64 control); two chains.
 // s_nop 1: a VALU write of v followed by a DPP read of it needs two wait states.
@@ -170,6 +193,13 @@ __device__ __forceinline__ double half_shift(double v) {
   const int lo = __builtin_amdgcn_update_dpp((int)b, (int)b, 0x12A, 0xC, 0xF, false);
   const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), 0x12A, 0xC, 0xF, false);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// v(lane l - 32) in the upper half (the lower half gets its own value back)
+__device__ __forceinline__ double other_half(double v) {
+  const long long b = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  return __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
 }
 // v(lane l) + v(lane l +- 16): rows 0 + 1 and rows 2 + 3, the same sum order in both rows
 __device__ __forceinline__ double row_pair_sum(double v) {
@@ -345,6 +375,11 @@ __device__ __forceinline__ double dyn_bound(const mpcq_params& p, const double* 
 // Shared memory of one instance (N=16: 40.4 KB -> 4 instances per CU;
 // N=32: 80.2 KB -> 2).
 
+// The sweep matrices (G / H / M^{-1} in GH, S^{-1} in Sm) are 12 x 12 with a row
+// stride of 13 doubles (26 banks): a row read (12 lanes, consecutive rows) and a
+// column read both touch distinct LDS banks.  GS = one stage's slot.
+constexpr int RS = 13, GS = 12 * RS;
+
 template <int N>
 struct Smem {
   double Ab[126 * N - 18];  // scaled constraint values, CSC order
@@ -352,8 +387,8 @@ struct Smem {
   // During the factorisation slot k holds Q_k [0,36), F_k W_k [36,108) and the
   // dynamics-row rho of stage k [108,120); during scaling the row factors; in
   // the prologue xref / fsteps / the gait walk.
-  double GH[N][144];
-  double Sm[N][144];        // S_k^{-1} / U_k^{-1} / M^{-1} of stage k, row-major
+  double GH[N][GS];
+  double Sm[N][GS];         // S_k^{-1} / U_k^{-1} of stage k, row-major (row stride RS)
   double FWs[N][72];        // F_k W_k (12x6, row psi at [6 psi]); W_k = B_k' R on rows 6..11
   double QL[N][36];         // B_k F_k W_k = R^{-1} W_k' F_k W_k (6x6)
   union {
@@ -363,7 +398,7 @@ struct Smem {
       double bo[N][12];
       double na[N][12];
       double nb[N][12];
-      double yv[N][12];      // sweep outputs y / v, then w = S^{-1} y in place
+      double yv[N][12];      // w = S^{-1} y of the inward sweep (states / duals during the checks)
       double xs[N + 1][12];  // X_k (xs[k+1] = X_{k+1}, stage k's states)
     } it;
     struct {
@@ -374,6 +409,8 @@ struct Smem {
   double dump[16 * N];      // per-lane sink: predicated stores write here instead of branching
   int flag[4];
 };
+// two instances share a CU's 160 KB at N = 16
+static_assert(sizeof(Smem<16>) <= 160 * 1024 / 2, "Smem<16> must leave room for two workgroups per CU");
 
 // prologue aliases inside GH
 template <int N>
@@ -670,8 +707,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 
     // ---- factorisation --------------------------------------------------------
     // dynamics-row rho of stage kk (published in GH[kk][108..120) at factor time)
-    auto rdy = [&](int kk, int i) __attribute__((always_inline)) { return GHr[144 * kk + 108 + i]; };
-    auto Qv = [&](int kk, int j1, int j2) __attribute__((always_inline)) { return GHr[144 * kk + 6 * j1 + j2]; };
+    auto rdy = [&](int kk, int i) __attribute__((always_inline)) { return GHr[GS * kk + 108 + i]; };
+    auto Qv = [&](int kk, int j1, int j2) __attribute__((always_inline)) { return GHr[GS * kk + 6 * j1 + j2]; };
     // The factorisation's row builders are branch-free: every load is unconditional
     // (indices clamped in range) and the structure is applied by selects.
     // The couplings are sparse: row i of L_kk (and column i) has its nonzeros on
@@ -841,7 +878,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           asm volatile("" ::: "memory");
         }
         if (cl) {
-          double* const Gd = &sh.GH[upper ? k : k + 1][12 * ph];
+          double* const Gd = &sh.GH[upper ? k : k + 1][RS * ph];
 #pragma unroll
           for (int ci = 0; ci < 12; ++ci) Gd[ci] = -G[ci];  // stored negated
         }
@@ -874,13 +911,13 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           gj12(Ro, ph, ok);
           if (cl) {
 #pragma unroll
-            for (int ci = 0; ci < 12; ++ci) sh.Sm[k][12 * ph + ci] = Ro[ci];
+            for (int ci = 0; ci < 12; ++ci) sh.Sm[k][RS * ph + ci] = Ro[ci];
           }
           wave_sync();  // the previous inverse has been consumed by this row
           if (cl) {
-            double* dst = mrow ? &sh.GH[0][0] : (bot ? Sb : St);
+            double* dst = mrow ? &sh.GH[0][RS * ph] : (bot ? Sb : St) + 12 * ph;
 #pragma unroll
-            for (int ci = 0; ci < 12; ++ci) dst[12 * ph + ci] = Ro[ci];
+            for (int ci = 0; ci < 12; ++ci) dst[ci] = Ro[ci];
           }
         }
         sync_all();
@@ -1238,117 +1275,111 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           }
           sync_all();
           STAMP(3);
-          // P5-P7: the state solve on wave 0 alone (no block barrier inside).  Rows
-          // 0 / 2 run the top-down sweep (columns 0-5 / 6-11 of each step's
-          // matrix), rows 1 / 3 the bottom-up one; the two halves of every product
-          // combine by permlane32_swap.  Inward, each step also forms
-          // w_k = S_k^{-1} y_k of the stage the previous step finished (off the
-          // dependency chain, sharing its broadcast); then the meeting stage and
-          // the outward sweeps.
-          const int half = (t >> 5) & 1, hoff = 6 * half;
+          // P5-P7: the state solve on wave 0 alone (no block barrier inside).
+          // Inward step j = 1..MID: top kk(j) = j, bottom kk(j) = N-1-j.  Half 0 (rows
+          // 0 top / 1 bottom) runs the recurrence y_kk = b_kk - G_kk y_kk(j-1) (G_kk of
+          // the top in GH[kk], H_kk of the bottom in GH[kk+1], stored negated), one
+          // full 12-term row per lane.  Half 1 (rows 2 / 3) runs the same instruction
+          // stream on S^{-1} rows two stages behind: w_kk(j-2) = S^{-1} y_kk(j-2), its y
+          // handed over by permlane32_swap.  Step MID+1 is the meeting stage: half 0
+          // solves x_m = M^{-1} (y_m + v_m - b_m) (top and bottom rows joined by
+          // permlane16_swap), half 1 the last top w.  Then the outward sweeps.
+          const int half = (t >> 5) & 1;
           auto bt_at = [&](lds_cd* q) __attribute__((always_inline)) {
             return (q[0] + q[12 * N]) + q[24 * N];
           };
           double xp = 0.0;
           if (t < 64) {
-            // Inward step j: top kk = j (G_kk in GH[kk]), bottom kk = N-1-j (H_kk in
-            // GH[kk+1]).  Pointers walk the stages (+-1 slot per step); the asm keeps
-            // them in registers so each step's loads stay in that step.
-            const int gs = cr == 0 ? 144 : -144, bs = cr == 0 ? 12 : -12;
-            lds_cd* GpN = GHr + 144 * (cr == 0 ? 1 : N - 1) + 12 * rr_ + hoff;  // G / H of step 1
-            lds_cd* BpN = (lds_cd*)&sh.u.it.bo[cr == 0 ? 0 : N - 1][rr_];        // bo; na, nb at +12N, +24N
-            lds_cd* SpN = SmR + 144 * (cr == 0 ? 0 : N - 1) + 12 * rr_ + hoff;  // S^{-1} of stage kk(0)
-            lds_d* Yp = (lds_d*)&sh.u.it.yv[cr == 0 ? 0 : N - 1][rr_];
-            double yp = bt_at(BpN);
+            const int gs = cr == 0 ? GS : -GS, bs = cr == 0 ? 12 : -12;
+            // rows of step 1: G / H (half 0); S^{-1} of stage kk(-1), never stored (half 1)
+            lds_cd* Mp = half == 0 ? GHr + (GS * (cr == 0 ? 1 : N - 1) + RS * rr_)
+                                   : SmR + (GS * (cr == 0 ? -1 : N) + RS * rr_);
+            lds_cd* BpN = (lds_cd*)&sh.u.it.bo[cr == 0 ? 0 : N - 1][rr_];  // bo; na, nb at +12N, +24N
+            lds_d* Yp = (lds_d*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? -1 : N) + rr_);  // w of kk(j-2)
+            double src = half == 0 ? bt_at(BpN) : 0.0;  // y_kk(0) (half 0)
             BpN += bs;
             // right-hand sides run two steps ahead: step j sums the one of step j+1
             // (loaded during step j-1) and loads the one of step j+2
             double bcn = bt_at(BpN);
             BpN += bs;
-            double g[6], sv[6], b0 = BpN[0], b1 = BpN[12 * N], b2 = BpN[24 * N];
+            double g[12], b0 = BpN[0], b1 = BpN[12 * N], b2 = BpN[24 * N];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) { g[i] = GpN[i]; sv[i] = SpN[i]; }
-            GpN += gs;
-            SpN += gs;
+            for (int i = 0; i < 12; ++i) g[i] = Mp[i];
+            Mp += gs;
             BpN += bs;
 #pragma unroll
-            for (int j = 1; j <= MID; ++j) {
-              asm volatile("" : "+v"(GpN), "+v"(SpN), "+v"(BpN), "+v"(Yp) : : "memory");
-              double gc[6], sc[6];
+            for (int j = 1; j <= MID + 1; ++j) {
+              asm volatile("" : "+v"(Mp), "+v"(BpN), "+v"(Yp) : : "memory");
+              double gc[12];
 #pragma unroll
-              for (int i = 0; i < 6; ++i) { gc[i] = g[i]; sc[i] = sv[i]; }
-              const double bc = bcn;
-              if (j < MID) {  // prefetch the next step's half rows
+              for (int i = 0; i < 12; ++i) gc[i] = g[i];
+              const double bc = j <= MID ? bcn : 0.0;
+              if (j < MID) {  // prefetch the next step's rows
 #pragma unroll
-                for (int i = 0; i < 6; ++i) { g[i] = GpN[i]; sv[i] = SpN[i]; }
-                GpN += gs;
-                SpN += gs;
-              } else {  // last step: the meeting stage's M^{-1} half row and right-hand side
+                for (int i = 0; i < 12; ++i) g[i] = Mp[i];
+                Mp += gs;
+              } else if (j == MID) {  // the meeting step: M^{-1} rows (half 0), the S walk (half 1)
+                lds_cd* q = half == 0 ? GHr + RS * rr_ : Mp;
 #pragma unroll
-                for (int i = 0; i < 6; ++i) g[i] = GHr[12 * rr_ + hoff + i];
-                lds_cd* q = (lds_cd*)&sh.u.it.bo[MID][rr_];
-                b0 = q[0]; b1 = q[12 * N]; b2 = q[24 * N];
+                for (int i = 0; i < 12; ++i) g[i] = q[i];
+                lds_cd* qb = (lds_cd*)&sh.u.it.bo[MID][rr_];
+                b0 = qb[0]; b1 = qb[12 * N]; b2 = qb[24 * N];
               }
               asm volatile("" : : : "memory");  // the prefetch is issued here, not sunk to its use
-              // y = b - G y_prev with -G stored: half 0 starts its chains from b
-              const double i0 = half == 0 ? bc : 0.0;
-              const double ys = half_shift(yp);
-              // the chain's products, then (off the chain) w of the stage the previous
-              // step finished (kk(j-1)), issued into the chain's latency
-              const double pa = bdot6(gc, ys, i0);
-              const double pw = bdot6(sc, ys, 0.0);
-              const double acc = pair_sum(pa);
+              double s_in = src;
+              if (j == MID + 1) s_in = half == 0 ? row_pair_sum(src) - ((b0 + b1) + b2) : src;
+              const double acc = bdot12(gc, s_in, half == 0 ? bc : 0.0);
               if (j < MID) bcn = (b0 + b1) + b2;
               if (j + 2 <= MID) {
                 b0 = BpN[0]; b1 = BpN[12 * N]; b2 = BpN[24 * N];
                 BpN += bs;
               }
-              const double wv = pair_sum(pw);
-              const bool wok = (cr == 0 || j == 1 || N - j >= MID) && (cr == 0 ? j - 1 : N - j) != MID;
-              *(wok && half == 0 && s < 12 ? Yp : (lds_d*)&sh.dump[t]) = wv;
+              if (j >= 2) {  // half 1: w of stage kk(j-2) (the meeting stage itself has none)
+                const bool wok = half == 1 && s < 12 && (j <= MID || cr == 0);
+                *(wok ? Yp : (lds_d*)&sh.dump[t]) = acc;
+              }
               Yp += bs;
-              yp = (cr == 0 || N - 1 - j >= MID) ? acc : yp;
-            }
-            // meeting stage: x_m = M^{-1} (y_m + v_m - b_m); the top (row 0 / 2) and
-            // bottom (row 1 / 3) results meet by permlane16_swap
-            {
-              const double cm = row_pair_sum(yp) - ((b0 + b1) + b2);
-              xp = pair_sum(bdot6(g, half_shift(cm), 0.0));
-              if (cr == 0 && half == 0 && s < 12) sh.u.it.xs[MID + 1][rr_] = xp;
+              if (j <= MID) {
+                const double up = other_half(src);  // half 1 receives y_kk(j-1)
+                const bool adv = cr == 0 || N - 1 - j >= MID;  // the bottom's step MID is idle
+                src = half == 0 ? (adv ? acc : src) : up;
+              } else {
+                xp = acc;
+                if (cr == 0 && half == 0 && s < 12) sh.u.it.xs[MID + 1][rr_] = xp;
+              }
             }
             STAMP(6);
-            // Outward step j: top kk = MID-j (G_{kk+1}' from GH[kk+1]), bottom kk = MID+j
-            // (H_{kk-1}' from GH[kk]); matrices read by column.  The bottom row's last
-            // step (kk = N) is idle: its loads stay inside the shared memory block and
-            // its store goes to the lane's sink.
-            const int ms = cr == 0 ? -144 : 144, ws = cr == 0 ? -12 : 12;
-            lds_cd* MpN = GHr + 144 * (cr == 0 ? MID : MID + 1) + rr_ + 12 * hoff;
+            // Outward step j: top kk = MID-j: X_kk = w_kk - G_{kk+1}' X_{kk+1} (G_{kk+1} in
+            // GH[kk+1]); bottom kk = MID+j: X_kk = w_kk - H_{kk-1}' X_{kk-1} (H_{kk-1} in
+            // GH[kk]).  Lane rr reads column rr (a full 12-term product per lane; half 1
+            // repeats half 0).  The bottom row's last step (kk = N) is idle: its loads stay
+            // inside the shared memory block and its store goes to the lane's sink.
+            const int ms = cr == 0 ? -GS : GS, ws = cr == 0 ? -12 : 12;
+            lds_cd* MpN = GHr + (GS * (cr == 0 ? MID : MID + 1) + rr_);
             lds_cd* WpN = (lds_cd*)&sh.u.it.yv[cr == 0 ? MID - 1 : MID + 1][rr_];
             lds_d* Xp = (lds_d*)&sh.u.it.xs[cr == 0 ? MID : MID + 2][rr_];
-            double bq;
 #pragma unroll
-            for (int i = 0; i < 6; ++i) g[i] = MpN[12 * i];
+            for (int i = 0; i < 12; ++i) g[i] = MpN[RS * i];
             MpN += ms;
-            wave_sync();  // the w written by the inward rows
-            bq = WpN[0];
+            wave_sync();  // the w written by half 1
+            double bq = WpN[0];
             WpN += ws;
 #pragma unroll
             for (int j = 1; j <= MID; ++j) {
               asm volatile("" : "+v"(MpN), "+v"(WpN), "+v"(Xp) : : "memory");
-              double gc[6];
+              double gc[12];
 #pragma unroll
-              for (int i = 0; i < 6; ++i) gc[i] = g[i];
+              for (int i = 0; i < 12; ++i) gc[i] = g[i];
               const double bc = bq;
               if (j < MID) {
 #pragma unroll
-                for (int i = 0; i < 6; ++i) g[i] = MpN[12 * i];
+                for (int i = 0; i < 12; ++i) g[i] = MpN[RS * i];
                 MpN += ms;
                 bq = WpN[0];
                 WpN += ws;
               }
               asm volatile("" : : : "memory");
-              const double i0 = half == 0 ? bc : 0.0;  // x = w - G' x_next with -G stored
-              const double acc = pair_sum(bdot6(gc, half_shift(xp), i0));
+              const double acc = bdot12(gc, xp, bc);  // x = w - G' x_next with -G stored
               const bool act = cr == 0 || MID + j <= N - 1;
               xp = act ? acc : xp;
               *(act && half == 0 && s < 12 ? Xp : (lds_d*)&sh.dump[t]) = acc;

@@ -958,12 +958,11 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     };
     // force column of A' v for own-row values v (dynamics rows 6..11 by row broadcast,
     // swing, friction by quad broadcast)
-    auto colF_off = [&](const double (&v)[3]) __attribute__((always_inline)) -> double {
+    auto colF_c = [&](const double (&A)[10], const double (&v)[3]) __attribute__((always_inline)) -> double {
       const double w6 = rbc<LN(6)>(v[0]), w7 = rbc<LN(7)>(v[0]), w8 = rbc<LN(8)>(v[0]);
       const double w9 = rbc<LN(9)>(v[0]), w10 = rbc<LN(10)>(v[0]), w11 = rbc<LN(11)>(v[0]);
       const double wf0 = qbc<0>(v[2]), wf1 = qbc<1>(v[2]), wf2 = qbc<2>(v[2]);
       const double wf3 = qbc<3>(v[0]), wf4 = qbc<3>(v[1]);
-      lds_cd* A = Ab + oF;
       double sA = A[0] * (cc == 0 ? w6 : (cc == 1 ? w7 : w8));
       double sB = A[1] * w9;
       sA += A[2] * w10;
@@ -973,6 +972,12 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       sA += A[6] * (cc == 1 ? wf3 : wf1);
       const double sC = (A[7] * wf2 + A[8] * wf3) + A[9] * wf4;  // friction rows 2..4 (cc == 2)
       return (sA + sB) + m2 * sC;
+    };
+    auto colF_off = [&](const double (&v)[3]) __attribute__((always_inline)) -> double {
+      double A[10];
+#pragma unroll
+      for (int i = 0; i < 10; ++i) A[i] = Ab[oF + i];
+      return colF_c(A, v);
     };
     // max over a 16-lane row: quad xor 1, xor 2, then rotations by 4 and 8
     auto row_max = [](double v) __attribute__((always_inline)) {
@@ -1248,26 +1253,33 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           // (stage-local, DPP only); then the sweep right-hand side of the own state
           // column (bo) and this stage's dynamics-row terms of stage k-1's state
           // columns (na, nb): the only LDS hand-off before the sweeps.
+          // every LDS operand of this phase is iteration-invariant: issue all the loads
+          // first (one LDS round trip instead of one per use)
+          double cf[10], fwc[12];
+#pragma unroll
+          for (int i = 0; i < 10; ++i) cf[i] = Ab[oF + i];
+#pragma unroll
+          for (int psi = 0; psi < 12; ++psi) fwc[psi] = FWr[oFWc + 6 * psi];
+          const double cXd = Ab[oXd], cHd = Ab[oHd], cH6 = Ab[oH6];
           double w[3];
 #pragma unroll
           for (int j = 0; j < 3; ++j) w[j] = rr[j] * z[j] - y[j];
-          const double bf = colF_off(w) + p.sigma * xf;  // b_f = sigma x_f + A_f' w (- q, q = 0)
+          // the phase's arithmetic starts after this point, the loads before it
+          asm volatile("" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]) : : "memory");
+          const double bf = colF_c(cf, w) + p.sigma * xf;  // b_f = sigma x_f + A_f' w (- q, q = 0)
           // u = F b_f (kept for the forces) and beta = R B u = (F W)' b_f (rows 6..11)
           double beta, uf;
           {
             double ball[12];
             gather12(bf, ball);
             uf = dot12(Fr, ball);
-            double fwc[12];
-#pragma unroll
-            for (int psi = 0; psi < 12; ++psi) fwc[psi] = FWr[oFWc + 6 * psi];
             beta = dot12(fwc, ball);
           }
           {
             const double wd = isv ? w[0] - beta : w[0];  // dynamics-row w less the force Schur term
-            const double bo = p.sigma * xX + Ab[oXd] * wd;
-            const double na = Ab[oHd] * wd;              // Hd(k, ph): on X_k[ph], stage k-1's column ph
-            const double nb = Ab[oH6] * w[0];            // H6(k, ph): on X_k[ph+6] (ph < 6)
+            const double bo = p.sigma * xX + cXd * wd;
+            const double na = cHd * wd;                  // Hd(k, ph): on X_k[ph], stage k-1's column ph
+            const double nb = cH6 * w[0];                // H6(k, ph): on X_k[ph+6] (ph < 6)
             // stage 0 zeroes the last stage's na / nb (that stage has no next stage)
             *(cl ? Wbo : Wdump) = bo;
             *(cl ? Wna : Wdump) = hp ? na : 0.0;
@@ -1391,17 +1403,23 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           // P8: forces f_k = F_k (b_f - R B' g) = u - (F W) g, with g = Xd X_{k+1} + Hd X_k
           // on the velocity rows (the states' part of those rows)
           double sf, sX, gm[6];
+          // all LDS operands of P8 / P9 first (one round trip)
           const double xa = XSr[oXSp], xb = XSr[oXSp6];
+          sX = XSr[oXS];
+          double fwl[6], qll[6];
+#pragma unroll
+          for (int i = 0; i < 6; ++i) { fwl[i] = FWr[oFW + i]; qll[i] = QLr[oQL + i]; }
+          const double eXd = Ab[oXd], eHd = Ab[oHd], eH6 = Ab[oH6];
+          const double cFb = Ab[oFb], cFa = Ab[oFa], cF4 = Ab[oF4], cSw = Ab[oF + 4];
+          asm volatile("" : : : "memory");
           {
-            sX = XSr[oXS];
-            const double g0 = Ab[oXd] * sX;
-            const double g1 = g0 + Ab[oHd] * xa;
+            const double g0 = eXd * sX;
+            const double g1 = g0 + eHd * xa;
             const double g = hp ? g1 : g0;  // used from the lanes of rows 6..11 only
             gm[0] = rbc<LN(6)>(g); gm[1] = rbc<LN(7)>(g); gm[2] = rbc<LN(8)>(g);
             gm[3] = rbc<LN(9)>(g); gm[4] = rbc<LN(10)>(g); gm[5] = rbc<LN(11)>(g);
-            lds_cd* fwr = FWr + oFW;
-            sf = uf - (((fwr[0] * gm[0] + fwr[2] * gm[2]) + fwr[4] * gm[4]) +
-                       ((fwr[1] * gm[1] + fwr[3] * gm[3]) + fwr[5] * gm[5]));
+            sf = uf - (((fwl[0] * gm[0] + fwl[2] * gm[2]) + fwl[4] * gm[4]) +
+                       ((fwl[1] * gm[1] + fwl[3] * gm[3]) + fwl[5] * gm[5]));
           }
           STAMP(9);
           // P9: z, y update (osqp update_z / update_y), x update.  A x~ on the own rows:
@@ -1409,19 +1427,18 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           {
             double ax[3];
             {
-              double dyn = Ab[oXd] * sX;
-              const double d1 = dyn + Ab[oHd] * xa;
-              const double d2 = d1 + Ab[oH6] * xb;
+              double dyn = eXd * sX;
+              const double d1 = dyn + eHd * xa;
+              const double d2 = d1 + eH6 * xb;
               dyn = hp ? (isv ? d1 : d2) : dyn;
-              lds_cd* ql = QLr + oQL;
-              const double bfv = beta * ri[0] - (((ql[0] * gm[0] + ql[2] * gm[2]) + ql[4] * gm[4]) +
-                                                 ((ql[1] * gm[1] + ql[3] * gm[3]) + ql[5] * gm[5]));
+              const double bfv = beta * ri[0] - (((qll[0] * gm[0] + qll[2] * gm[2]) + qll[4] * gm[4]) +
+                                                 ((qll[1] * gm[1] + qll[3] * gm[3]) + qll[5] * gm[5]));
               dyn = isv ? dyn + bfv : dyn;
               // friction rows: lane c < 3 owns row c, lane 3 rows 3 and 4 (all loads unconditional)
               const double q0 = qbc<0>(sf), q1 = qbc<1>(sf), q2 = qbc<2>(sf);
-              const double frA = Ab[oFb] * q2 + Ab[oFa] * (ta0 ? q0 : q1);
-              const double frB = Ab[oF4] * q2;
-              const double swg = Ab[oF + 4] * sf;
+              const double frA = cFb * q2 + cFa * (ta0 ? q0 : q1);
+              const double frB = cF4 * q2;
+              const double swg = cSw * sf;
               ax[0] = cl ? dyn : frA;
               ax[1] = cl ? swg : frB;
               ax[2] = cl ? frA : 0.0;

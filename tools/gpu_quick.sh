@@ -11,4 +11,5 @@ echo "pytest rc=$rc" >> $OUT/pytest_$TAG.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python tools/stamps.py > $OUT/stamps_$TAG.log 2>&1 &&
 timeout -k 10 300 python tools/stamps.py --batch 256 >> $OUT/stamps_$TAG.log 2>&1 &&
-timeout -k 10 600 python bench.py --cpu-sample 256 > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
+timeout -k 10 600 python bench.py --cpu-sample 256 > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err &&
+timeout -k 10 300 python tools/iterbench.py > $OUT/iter_$TAG.txt 2>&1

@@ -1,0 +1,61 @@
+"""Per-iteration latency of the production kernel, free of the batch's tail effects.
+
+    python tools/iterbench.py [--N 16] [--reps 5]
+
+Takes the C2 batch (bench.py's seeded synthetic instances), finds its slowest
+instance and launches B identical copies of it (B = 256: one instance per CU;
+512: two, the bench's occupancy; 1024: two resident, two rounds).  Every copy
+runs the same iterations, so kernel time / iterations is the per-iteration
+latency at that occupancy.
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "mpc-tsid_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--N", type=int, default=16)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    import torch
+    import mpcq
+    dev = torch.device("cuda", 0)
+    eng = mpcq.Engine(a.N)
+    src = mpcq.synth.make_batch(1024, a.N, gaits=("trot",), seed=2)  # bench.py C2 data
+
+    def run(xref, fsteps, reps):
+        B = xref.shape[0]
+        xr = torch.from_numpy(np.ascontiguousarray(xref)).to(dev)
+        fs = torch.from_numpy(np.ascontiguousarray(fsteps)).to(dev)
+        f0 = torch.empty((B, 12), dtype=torch.float64, device=dev)
+        st = torch.empty(B, dtype=torch.int32, device=dev)
+        it = torch.empty(B, dtype=torch.int32, device=dev)
+        ms = []
+        for _ in range(reps):
+            eng.solve_device(B, xr.data_ptr(), fs.data_ptr(), f0.data_ptr(), st.data_ptr(), it.data_ptr())
+            torch.cuda.synchronize()
+            ms.append(eng.last_kernel_ms()[1])
+        return it.cpu().numpy(), float(np.median(ms))
+
+    its, ms = run(src["xref"], src["fsteps"], a.reps)
+    slow = int(np.argmax(its))
+    print(f"C2 batch: kernel {ms:.3f} ms, iterations median {np.median(its):.0f} max {its.max()} (instance {slow})")
+    for B in (256, 512, 1024):
+        xr = np.repeat(src["xref"][slow:slow + 1], B, axis=0)
+        fs = np.repeat(src["fsteps"][slow:slow + 1], B, axis=0)
+        it2, ms2 = run(xr, fs, a.reps)
+        assert (it2 == it2[0]).all()
+        n_it = int(it2[0])
+        print(f"B={B:5d} copies of the slowest: {ms2:8.3f} ms, {n_it} iterations, "
+              f"{1e3 * ms2 / n_it:7.3f} us/iteration")
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -58,6 +58,9 @@ def main():
     fetch = counters(os.path.join(src, "fetch", "run_counter_collection.csv"))
     write = counters(os.path.join(src, "write", "run_counter_collection.csv"))
     sq = counters(os.path.join(src, "sq", "run_counter_collection.csv"))
+    for k2, v2 in counters(os.path.join(src, "sq2", "run_counter_collection.csv")).items():
+        if k2 != "SQ_WAVES":
+            sq[k2] = v2
 
     fk, wk = mean(fetch.get("FETCH_SIZE", [])), mean(write.get("WRITE_SIZE", []))
     traffic = None
@@ -82,12 +85,13 @@ def main():
         cyc = mean(sq.get("SQ_WAVE_CYCLES", [])) or 0.0
         lines += ["", "## SQ counters (per launch; *_CYCLES and WAIT/ACTIVE in quad-cycles)", ""]
         for name in ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
-                     "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU"):
+                     "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",
+                     "SQ_ACTIVE_INST_SCA", "SQ_WAIT_INST_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_BUSY_CYCLES"):
             v = mean(sq.get(name, []))
             if v is None:
                 continue
             extra = f" ({v / w:.4g} per wave)"
-            if name.startswith("SQ_WAIT") or name == "SQ_ACTIVE_INST_ANY":
+            if name.startswith("SQ_WAIT") or name.startswith("SQ_ACTIVE_INST"):
                 extra += f", {100 * v / cyc:.1f} % of wave cycles" if cyc else ""
             lines.append(f"- {name}: {v:.4g}{extra}")
     open(os.path.join(dst, f"{a.tag}_summary.md"), "w").write("\n".join(lines) + "\n")

@@ -42,6 +42,8 @@ namespace {
 // invariant values into registers.
 typedef __attribute__((address_space(3))) const double lds_cd;
 typedef __attribute__((address_space(3))) double lds_d;
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const dbl2 lds_cd2;
 
 constexpr double kInf = 1e30;  // OSQP_INFTY
 constexpr double kMinScaling = 1e-4, kMaxScaling = 1e4;
@@ -99,45 +101,35 @@ __device__ __forceinline__ double rbc(double v) { return dppd<0x150 + J>(v); }
 template <int J>
 __device__ __forceinline__ double qbc(double v) { return dppd<85 * J>(v); }
 
-// i0 + sum_{j<12} g_j * v_j, v_j broadcast from lane j of the row (v_fmac_f64_dpp);
-// two interleaved chains.  s_nop 1: a VALU write of v then a DPP read of it needs two
-// wait states.
+// i0 + sum_{j<12} g_j * v_j, v_j broadcast from lane j of the row (v_fmac_f64_dpp).
+// One dependent chain: the fmac issue interval exceeds its latency.  s_nop 1: a VALU
+// write of v then a DPP read of it needs two wait states.
 __device__ __forceinline__ double bdot12(const double (&g)[12], double v, double i0) {
-  double a0 = i0, a1 = 0.0;
+  double a0 = i0;
   asm volatile("s_nop 1\n\t"
-      "v_fmac_f64_dpp %0, %2, %3 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %1, %2, %4 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %0, %2, %5 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %1, %2, %6 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %0, %2, %7 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %1, %2, %8 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %0, %2, %9 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %1, %2, %10 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %0, %2, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %1, %2, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %0, %2, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %1, %2, %14 row_newbcast:11 row_mask:0xf bank_mask:0xf"
-      : "+v"(a0), "+v"(a1)
+      "v_fmac_f64_dpp %0, %1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %3 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %4 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %5 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %6 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %7 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %8 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %9 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %10 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %12 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %13 row_newbcast:11 row_mask:0xf bank_mask:0xf"
+      : "+v"(a0)
       : "v"(v), "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]), "v"(g[4]), "v"(g[5]), "v"(g[6]), "v"(g[7]),
         "v"(g[8]), "v"(g[9]), "v"(g[10]), "v"(g[11]));
-  return a0 + a1;
+  return a0;
 }
-// i0 + sum_{j<6} g_j * v_j with v_j broadcast from lane j of the row, the broadcasts
-// folded into v_fmac_f64_dpp (row_newbcast is the one DPP64 control); two chains.
-// s_nop 1: a VALU write of v followed by a DPP read of it needs two wait states.
-__device__ __forceinline__ double bdot6(const double (&g)[6], double v, double i0) {
-  double a0 = i0, a1 = 0.0;
-  // volatile: stays after the sweeps' prefetch fences, so the loads issue first
-  asm volatile("s_nop 1\n\t"
-      "v_fmac_f64_dpp %0, %2, %3 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %1, %2, %4 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %0, %2, %5 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %1, %2, %6 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %0, %2, %7 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %1, %2, %8 row_newbcast:5 row_mask:0xf bank_mask:0xf"
-      : "+v"(a0), "+v"(a1)
-      : "v"(v), "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]), "v"(g[4]), "v"(g[5]));
-  return a0 + a1;
+// lower half: keep a; upper half: b of lane l - 32 (one permlane32_swap per dword)
+__device__ __forceinline__ double keep_lo_take_lo(double a, double b) {
+  const long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)y, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(x >> 32), (unsigned)(y >> 32), false, false);
+  return __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
 }
 
 template <int... J>
@@ -156,26 +148,6 @@ __device__ __forceinline__ void gatherd_seq(double v, double (&all)[12], std::in
 __device__ __forceinline__ void gather_direct12(double v, double (&all)[12]) {
   gatherd_seq(v, all, std::make_integer_sequence<int, 12>{});
 }
-// sum_j M[j * stride] * v_j with v_j broadcast from lane j of the row (three chains for ILP)
-template <int... J>
-__device__ __forceinline__ double dotb_seq(lds_cd* M, int stride, double v, std::integer_sequence<int, J...>) {
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-  (((J % 3 == 0 ? a0 : (J % 3 == 1 ? a1 : a2)) += M[J * stride] * rbc<J>(v)), ...);
-  return (a0 + a1) + a2;
-}
-__device__ __forceinline__ double dotb12(lds_cd* M, int stride, double v) {
-  return dotb_seq(M, stride, v, std::make_integer_sequence<int, 12>{});
-}
-template <int... J>
-__device__ __forceinline__ double dotr_seq(const double (&g)[12], double v, std::integer_sequence<int, J...>) {
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-  (((J % 3 == 0 ? a0 : (J % 3 == 1 ? a1 : a2)) += g[J] * rbc<J>(v)), ...);
-  return (a0 + a1) + a2;
-}
-// sum_j g_j * v_j, v_j broadcast from lane j of the row
-__device__ __forceinline__ double dotr12(const double (&g)[12], double v) {
-  return dotr_seq(g, v, std::make_integer_sequence<int, 12>{});
-}
 // sum_j a_j b_j over 12 terms in three interleaved chains (shorter dependency path)
 __device__ __forceinline__ double dot12(const double (&a)[12], const double (&b)[12]) {
   double s0 = a[0] * b[0], s1 = a[1] * b[1], s2 = a[2] * b[2];
@@ -186,20 +158,6 @@ __device__ __forceinline__ double dot12(const double (&a)[12], const double (&b)
     s2 += a[j + 2] * b[j + 2];
   }
   return (s0 + s1) + s2;
-}
-// rows 2 and 3 of the wave take lane r+6 of their own row (row_ror:10); rows 0, 1 keep v
-__device__ __forceinline__ double half_shift(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp((int)b, (int)b, 0x12A, 0xC, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), 0x12A, 0xC, 0xF, false);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-// v(lane l - 32) in the upper half (the lower half gets its own value back)
-__device__ __forceinline__ double other_half(double v) {
-  const long long b = __double_as_longlong(v);
-  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
-  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
-  return __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
 }
 // v(lane l) + v(lane l +- 16): rows 0 + 1 and rows 2 + 3, the same sum order in both rows
 __device__ __forceinline__ double row_pair_sum(double v) {
@@ -224,36 +182,11 @@ __device__ __forceinline__ double pair_max(double v) {
   return fmax(__longlong_as_double(((long long)hi[0] << 32) | lo[0]),
               __longlong_as_double(((long long)hi[1] << 32) | lo[1]));
 }
-// v(lane l) + v(lane l +- 32): rows 0 + 2 and rows 1 + 3, the same sum order in both halves
-__device__ __forceinline__ double pair_sum(double v) {
-  const long long b = __double_as_longlong(v);
-  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
-  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
-  const double a0 = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
-  const double a1 = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
-  return a0 + a1;
-}
-template <int... J>
-__device__ __forceinline__ double dot6_seq(const double (&g)[6], double v, std::integer_sequence<int, J...>) {
-  double a0 = 0.0, a1 = 0.0;
-  (((J % 2 == 0 ? a0 : a1) += g[J] * rbc<J>(v)), ...);
-  return a0 + a1;
-}
-// sum_{i<6} g_i * v_i, v_i broadcast from lane i of the row
-__device__ __forceinline__ double dot6(const double (&g)[6], double v) {
-  return dot6_seq(g, v, std::make_integer_sequence<int, 6>{});
-}
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-  return v;
-}
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
-// a wave-uniform double kept in SGPRs
 // Launder an LDS base pointer: the pointer round-trips a VGPR through an empty asm
 // (opaque to the optimiser, so loads through it are not hoisted out of loops)
 // and comes back uniform in an SGPR via readfirstlane, costing no VGPR.
@@ -263,6 +196,7 @@ __device__ __forceinline__ void lds_uniform(P*& q) {
   q = reinterpret_cast<P*>(static_cast<unsigned long>(
       __builtin_amdgcn_readfirstlane(static_cast<int>(reinterpret_cast<unsigned long>(q)))));
 }
+// a wave-uniform double kept in SGPRs
 __device__ __forceinline__ double uni(double v) {
   const long long bits = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readfirstlane((int)bits);
@@ -378,7 +312,7 @@ __device__ __forceinline__ double dyn_bound(const mpcq_params& p, const double* 
 // The sweep matrices (G / H / M^{-1} in GH, S^{-1} in Sm) are 12 x 12 with a row
 // stride of 13 doubles (26 banks): a row read (12 lanes, consecutive rows) and a
 // column read both touch distinct LDS banks.  GS = one stage's slot.
-constexpr int RS = 13, GS = 12 * RS;
+constexpr int RS = 12, GS = 12 * RS;
 
 template <int N>
 struct Smem {
@@ -387,8 +321,8 @@ struct Smem {
   // During the factorisation slot k holds Q_k [0,36), F_k W_k [36,108) and the
   // dynamics-row rho of stage k [108,120); during scaling the row factors; in
   // the prologue xref / fsteps / the gait walk.
-  double GH[N][GS];
-  double Sm[N][GS];         // S_k^{-1} / U_k^{-1} of stage k, row-major (row stride RS)
+  alignas(16) double GH[N][GS];
+  alignas(16) double Sm[N][GS];         // S_k^{-1} / U_k^{-1} of stage k, row-major (row stride RS)
   double FWs[N][72];        // F_k W_k (12x6, row psi at [6 psi]); W_k = B_k' R on rows 6..11
   double QL[N][36];         // B_k F_k W_k = R^{-1} W_k' F_k W_k (6x6)
   union {
@@ -1300,6 +1234,11 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           auto bt_at = [&](lds_cd* q) __attribute__((always_inline)) {
             return (q[0] + q[12 * N]) + q[24 * N];
           };
+#ifndef MPCQ_REP_SWEEP
+#define MPCQ_REP_SWEEP 1
+#endif
+#pragma nounroll
+          for (int rep_ = 0; rep_ < MPCQ_REP_SWEEP; ++rep_) {  // > 1: timing experiments only
           double xp = 0.0;
           if (t < 64) {
             const int gs = cr == 0 ? GS : -GS, bs = cr == 0 ? 12 : -12;
@@ -1311,12 +1250,21 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             double src = half == 0 ? bt_at(BpN) : 0.0;  // y_kk(0) (half 0)
             BpN += bs;
             // right-hand sides run two steps ahead: step j sums the one of step j+1
-            // (loaded during step j-1) and loads the one of step j+2
-            double bcn = bt_at(BpN);
+            // (loaded during step j-1) and loads the one of step j+2; half 1 (the w
+            // products) starts its chain from 0
+            const double m0 = half == 0 ? 1.0 : 0.0;
+            double bcn = bt_at(BpN) * m0;
             BpN += bs;
             double g[12], b0 = BpN[0], b1 = BpN[12 * N], b2 = BpN[24 * N];
+            auto row12 = [&](lds_cd* q) __attribute__((always_inline)) {  // 16-B aligned row: 6 ds_read_b128
 #pragma unroll
-            for (int i = 0; i < 12; ++i) g[i] = Mp[i];
+              for (int i = 0; i < 6; ++i) {
+                const dbl2 v = ((lds_cd2*)q)[i];
+                g[2 * i] = v.x;
+                g[2 * i + 1] = v.y;
+              }
+            };
+            row12(Mp);
             Mp += gs;
             BpN += bs;
 #pragma unroll
@@ -1327,21 +1275,18 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               for (int i = 0; i < 12; ++i) gc[i] = g[i];
               const double bc = j <= MID ? bcn : 0.0;
               if (j < MID) {  // prefetch the next step's rows
-#pragma unroll
-                for (int i = 0; i < 12; ++i) g[i] = Mp[i];
+                row12(Mp);
                 Mp += gs;
               } else if (j == MID) {  // the meeting step: M^{-1} rows (half 0), the S walk (half 1)
-                lds_cd* q = half == 0 ? GHr + RS * rr_ : Mp;
-#pragma unroll
-                for (int i = 0; i < 12; ++i) g[i] = q[i];
+                row12(half == 0 ? GHr + RS * rr_ : Mp);
                 lds_cd* qb = (lds_cd*)&sh.u.it.bo[MID][rr_];
                 b0 = qb[0]; b1 = qb[12 * N]; b2 = qb[24 * N];
               }
               asm volatile("" : : : "memory");  // the prefetch is issued here, not sunk to its use
               double s_in = src;
               if (j == MID + 1) s_in = half == 0 ? row_pair_sum(src) - ((b0 + b1) + b2) : src;
-              const double acc = bdot12(gc, s_in, half == 0 ? bc : 0.0);
-              if (j < MID) bcn = (b0 + b1) + b2;
+              const double acc = bdot12(gc, s_in, bc);
+              if (j < MID) bcn = ((b0 + b1) + b2) * m0;
               if (j + 2 <= MID) {
                 b0 = BpN[0]; b1 = BpN[12 * N]; b2 = BpN[24 * N];
                 BpN += bs;
@@ -1352,9 +1297,10 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               }
               Yp += bs;
               if (j <= MID) {
-                const double up = other_half(src);  // half 1 receives y_kk(j-1)
-                const bool adv = cr == 0 || N - 1 - j >= MID;  // the bottom's step MID is idle
-                src = half == 0 ? (adv ? acc : src) : up;
+                // half 0 continues with y_kk(j) (the bottom's step MID is idle), half 1
+                // receives y_kk(j-1) from half 0
+                const bool adv = cr == 0 || N - 1 - j >= MID;
+                src = keep_lo_take_lo(adv ? acc : src, src);
               } else {
                 xp = acc;
                 if (cr == 0 && half == 0 && s < 12) sh.u.it.xs[MID + 1][rr_] = xp;
@@ -1398,6 +1344,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               Xp += ws;
             }
           }
+          wave_sync();
+          }  // MPCQ_REP_SWEEP
           sync_all();
           STAMP(7);
           // P8: forces f_k = F_k (b_f - R B' g) = u - (F W) g, with g = Xd X_{k+1} + Hd X_k

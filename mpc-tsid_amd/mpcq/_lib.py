@@ -12,8 +12,9 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # MPCQ_LIB_VARIANT=stamps loads the diagnostic build (per-phase cycle stamps)
-LIB_PATH = os.path.join(HERE, "libmpcq_stamps.so" if os.environ.get("MPCQ_LIB_VARIANT") == "stamps"
-                        else "libmpcq.so")
+# (any other MPCQ_LIB_VARIANT=<v> loads libmpcq_<v>.so, an experiment build)
+_VARIANT = os.environ.get("MPCQ_LIB_VARIANT")
+LIB_PATH = os.path.join(HERE, f"libmpcq_{_VARIANT}.so" if _VARIANT else "libmpcq.so")
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 
 # return codes / status / flags / modes (include/mpcq.h)

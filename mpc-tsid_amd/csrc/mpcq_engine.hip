@@ -53,7 +53,14 @@ constexpr double kDivTol = 1e-30;
 // constraint classes (OSQP set_rho_vec)
 enum : unsigned { RC_LOOSE = 0, RC_INEQ = 1, RC_EQ = 2 };
 
-#ifdef MPCQ_STAMPS
+#if defined(MPCQ_STAMPS) && defined(MPCQ_STAMPS_LEAN)
+// lean variant: only the uniform points after the loop's barriers (1 prologue, 2 factor,
+// 3 P1-P4, 7 sweeps, 10 P8-P9, 11 checks, 12 epilogue), accumulated in SGPRs without a
+// lane branch, so the measured code stays close to the production build
+#define STAMP_DECL uint64_t st_acc[16] = {}; uint64_t st_last = __builtin_amdgcn_s_memtime();
+#define STAMP(i) do { if constexpr ((i) == 1 || (i) == 2 || (i) == 3 || (i) == 7 || (i) == 10 || (i) == 11 || (i) == 12) { \
+    const uint64_t nw_ = __builtin_amdgcn_s_memtime(); st_acc[i] += nw_ - st_last; st_last = nw_; } } while (0)
+#elif defined(MPCQ_STAMPS)
 #define STAMP_DECL uint64_t st_acc[16] = {}; uint64_t st_last = __builtin_amdgcn_s_memtime();
 #define STAMP(i) do { if (threadIdx.x == 0) { const uint64_t nw_ = __builtin_amdgcn_s_memtime(); st_acc[i] += nw_ - st_last; st_last = nw_; } } while (0)
 #else
@@ -122,6 +129,42 @@ __device__ __forceinline__ double bdot12(const double (&g)[12], double v, double
       : "+v"(a0)
       : "v"(v), "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]), "v"(g[4]), "v"(g[5]), "v"(g[6]), "v"(g[7]),
         "v"(g[8]), "v"(g[9]), "v"(g[10]), "v"(g[11]));
+  return a0;
+}
+// i0 + sum_psi g_psi * v(lane LN(psi)) over a stage's 12 force / state slots, the
+// broadcasts folded into v_fmac_f64_dpp (one chain; s_nop 1 covers the DPP read hazard).
+__device__ __forceinline__ double bdot_ln12(const double (&g)[12], double v, double i0) {
+  double a0 = i0;
+  asm("s_nop 1\n\t"
+      "v_fmac_f64_dpp %0, %1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %3 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %4 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %5 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %6 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %7 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %8 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %9 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %11 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %12 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %13 row_newbcast:14 row_mask:0xf bank_mask:0xf"
+      : "+v"(a0)
+      : "v"(v), "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]), "v"(g[4]), "v"(g[5]), "v"(g[6]), "v"(g[7]),
+        "v"(g[8]), "v"(g[9]), "v"(g[10]), "v"(g[11]));
+  return a0;
+}
+// i0 + sum_i g_i * v(lane LN(6 + i)), i < 6: the velocity slots
+__device__ __forceinline__ double bdot_ln6v(const double (&g)[6], double v, double i0) {
+  double a0 = i0;
+  asm("s_nop 1\n\t"
+      "v_fmac_f64_dpp %0, %1, %2 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %3 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %4 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %5 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %6 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %7 row_newbcast:14 row_mask:0xf bank_mask:0xf"
+      : "+v"(a0)
+      : "v"(v), "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]), "v"(g[4]), "v"(g[5]));
   return a0;
 }
 // lower half: keep a; upper half: b of lane l - 32 (one permlane32_swap per dword)
@@ -571,6 +614,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     unsigned cls = 0u;
     double cscale = 1.0;
     int it_done = 0, n_upd = 0;
+#ifdef MPCQ_FACTIME
+    uint64_t fac_cycles = 0;
+#endif
     double rho_s = a.rho_in ? a.rho_in[b] : p.rho;
     rho_s = fmin(fmax(rho_s, kRhoMin), kRhoMax);
 
@@ -935,15 +981,14 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       {  // primal side: A x - z on the own rows
         double ax[3], q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         {
-          double fall[12], bco[12];
-          gather12(xf, fall);
+          double bco[12];
 #pragma unroll
           for (int psi = 0; psi < 12; ++psi) {
             const int fp = psi / 3, cp = psi % 3;
             const double v = Ab[oB0 + 24 * fp + 7 * cp];
             bco[psi] = (ph >= 9 || (isv && cp == ph - 6)) ? v : 0.0;
           }
-          const double bfx = dot12(bco, fall);
+          const double bfx = bdot_ln12(bco, xf, 0.0);
           double dyn = Ab[oXd] * xX;
           const double d1 = dyn + Ab[oHd] * YV[oXSp - 12];
           const double d2 = d1 + Ab[oH6] * YV[oXSp6 - 12];
@@ -1178,7 +1223,19 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma unroll
       for (int j = 0; j < 3; ++j) { lo[j] = lo_of(j); hi[j] = hi_of(j); }
       for (;;) {
-        if (!factor(p.sigma)) { status = MPCQ_STATUS_FACTOR_FAILED; break; }
+#ifndef MPCQ_REP_FACTOR
+#define MPCQ_REP_FACTOR 1
+#endif
+        bool fac_ok = true;
+#ifdef MPCQ_FACTIME
+        const uint64_t ft0_ = __builtin_amdgcn_s_memtime();
+#endif
+#pragma nounroll
+        for (int rep_ = 0; rep_ < MPCQ_REP_FACTOR; ++rep_) fac_ok = factor(p.sigma);  // > 1: timing only
+#ifdef MPCQ_FACTIME
+        fac_cycles += __builtin_amdgcn_s_memtime() - ft0_;
+#endif
+        if (!fac_ok) { status = MPCQ_STATUS_FACTOR_FAILED; break; }
         STAMP(2);
         bool refactor = false;
         for (; iter <= p.max_iter; ++iter) {
@@ -1202,13 +1259,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           asm volatile("" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]) : : "memory");
           const double bf = colF_c(cf, w) + p.sigma * xf;  // b_f = sigma x_f + A_f' w (- q, q = 0)
           // u = F b_f (kept for the forces) and beta = R B u = (F W)' b_f (rows 6..11)
-          double beta, uf;
-          {
-            double ball[12];
-            gather12(bf, ball);
-            uf = dot12(Fr, ball);
-            beta = dot12(fwc, ball);
-          }
+          const double uf = bdot_ln12(Fr, bf, 0.0);
+          const double beta = bdot_ln12(fwc, bf, 0.0);
           {
             const double wd = isv ? w[0] - beta : w[0];  // dynamics-row w less the force Schur term
             const double bo = p.sigma * xX + cXd * wd;
@@ -1350,7 +1402,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           STAMP(7);
           // P8: forces f_k = F_k (b_f - R B' g) = u - (F W) g, with g = Xd X_{k+1} + Hd X_k
           // on the velocity rows (the states' part of those rows)
-          double sf, sX, gm[6];
+          double sf, sX, gv;
           // all LDS operands of P8 / P9 first (one round trip)
           const double xa = XSr[oXSp], xb = XSr[oXSp6];
           sX = XSr[oXS];
@@ -1363,11 +1415,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           {
             const double g0 = eXd * sX;
             const double g1 = g0 + eHd * xa;
-            const double g = hp ? g1 : g0;  // used from the lanes of rows 6..11 only
-            gm[0] = rbc<LN(6)>(g); gm[1] = rbc<LN(7)>(g); gm[2] = rbc<LN(8)>(g);
-            gm[3] = rbc<LN(9)>(g); gm[4] = rbc<LN(10)>(g); gm[5] = rbc<LN(11)>(g);
-            sf = uf - (((fwl[0] * gm[0] + fwl[2] * gm[2]) + fwl[4] * gm[4]) +
-                       ((fwl[1] * gm[1] + fwl[3] * gm[3]) + fwl[5] * gm[5]));
+            gv = hp ? g1 : g0;  // used from the lanes of rows 6..11 only
+            sf = uf - bdot_ln6v(fwl, gv, 0.0);
           }
           STAMP(9);
           // P9: z, y update (osqp update_z / update_y), x update.  A x~ on the own rows:
@@ -1379,8 +1428,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               const double d1 = dyn + eHd * xa;
               const double d2 = d1 + eH6 * xb;
               dyn = hp ? (isv ? d1 : d2) : dyn;
-              const double bfv = beta * ri[0] - (((qll[0] * gm[0] + qll[2] * gm[2]) + qll[4] * gm[4]) +
-                                                 ((qll[1] * gm[1] + qll[3] * gm[3]) + qll[5] * gm[5]));
+              const double bfv = beta * ri[0] - bdot_ln6v(qll, gv, 0.0);
               dyn = isv ? dyn + bfv : dyn;
               // friction rows: lane c < 3 owns row c, lane 3 rows 3 and 4 (all loads unconditional)
               const double q0 = qbc<0>(sf), q1 = qbc<1>(sf), q2 = qbc<2>(sf);
@@ -1469,7 +1517,11 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       if (a.info) {
         a.info[4 * b + 0] = n_upd;
         a.info[4 * b + 1] = 0;
+#ifdef MPCQ_FACTIME
+        a.info[4 * b + 2] = (int)(fac_cycles >> 8);  // factorisation cycles / 256 (timing build)
+#else
         a.info[4 * b + 2] = 0;
+#endif
         a.info[4 * b + 3] = 0;
       }
     }

@@ -45,7 +45,9 @@ def main():
 
     its, ms = run(src["xref"], src["fsteps"], a.reps)
     slow = int(np.argmax(its))
-    print(f"C2 batch: kernel {ms:.3f} ms, iterations median {np.median(its):.0f} max {its.max()} (instance {slow})")
+    r = eng.solve(src["xref"][slow:slow + 1], src["fsteps"][slow:slow + 1])
+    print(f"C2 batch: kernel {ms:.3f} ms, iterations median {np.median(its):.0f} max {its.max()} (instance {slow}, "
+          f"{int(r['rho_updates'][0])} rho updates)")
     for B in (256, 512, 1024):
         xr = np.repeat(src["xref"][slow:slow + 1], B, axis=0)
         fs = np.repeat(src["fsteps"][slow:slow + 1], B, axis=0)

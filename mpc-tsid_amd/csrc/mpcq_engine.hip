@@ -384,6 +384,7 @@ struct Smem {
   } u;
   double red[12 * N];  // per-row partial reductions
   double dump[16 * N];      // per-lane sink: predicated stores write here instead of branching
+  double zero[72];          // zeros: masked coefficient reads point here instead of selecting
   int flag[4];
 };
 // two instances share a CU's 160 KB at N = 16
@@ -484,6 +485,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
   double bnd = 0.0;
   double lo_g[FUSED ? 1 : 3], hi_g[FUSED ? 1 : 3];
   if (t == 0) { sh.flag[0] = 0; sh.flag[1] = 0; sh.flag[2] = 0; sh.flag[3] = 0; }
+  if (t < 72) sh.zero[t] = 0.0;
+  if (t < 12) sh.u.it.xs[0][t] = 0.0;  // X_0 slot (masked reads multiply it by zero)
 
   // ---------------------------------------------------------------- prologue
   if (FUSED || !SOLVE) {
@@ -927,6 +930,13 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     const int oQL = 36 * k + 6 * (isv ? ph - 6 : 0);
     const int oXS = 12 * (k + 1) + ph, oXSp = 12 * k + ph, oXSp6 = 12 * k + (ph < 6 ? ph + 6 : ph);
     const double m2 = cc == 2 ? 1.0 : 0.0;
+    // masked variants for the loop: a lane whose term is structurally absent reads a
+    // zero (stage 0 has no previous stage; H6 only on the position rows; the force Schur
+    // terms beta, (R^-1 Q) g only on the velocity rows), so no selects are needed
+    const int oHdm = hp ? oHd : (int)(sh.zero - sh.Ab);
+    const int oH6m = hp && !isv ? oH6 : (int)(sh.zero - sh.Ab);
+    const int oFWcm = isv ? oFWc : (int)(sh.zero - &sh.FWs[0][0]);
+    const int oQLm = isv ? oQL : (int)(sh.zero - &sh.QL[0][0]);
     lds_cd* XSr = (lds_cd*)&sh.u.it.xs[0][0];
     double* const Wbo = &sh.u.it.bo[k][ph];
     double* const Wna = &sh.u.it.na[hp ? k - 1 : N - 1][ph];
@@ -1250,8 +1260,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma unroll
           for (int i = 0; i < 10; ++i) cf[i] = Ab[oF + i];
 #pragma unroll
-          for (int psi = 0; psi < 12; ++psi) fwc[psi] = FWr[oFWc + 6 * psi];
-          const double cXd = Ab[oXd], cHd = Ab[oHd], cH6 = Ab[oH6];
+          for (int psi = 0; psi < 12; ++psi) fwc[psi] = FWr[oFWcm + 6 * psi];
+          const double cXd = Ab[oXd], cHd = Ab[oHdm], cH6 = Ab[oH6m];
           double w[3];
 #pragma unroll
           for (int j = 0; j < 3; ++j) w[j] = rr[j] * z[j] - y[j];
@@ -1262,14 +1272,15 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           const double uf = bdot_ln12(Fr, bf, 0.0);
           const double beta = bdot_ln12(fwc, bf, 0.0);
           {
-            const double wd = isv ? w[0] - beta : w[0];  // dynamics-row w less the force Schur term
+            const double wd = w[0] - beta;  // dynamics-row w less the force Schur term (beta = 0 on rows 0..5)
             const double bo = p.sigma * xX + cXd * wd;
             const double na = cHd * wd;                  // Hd(k, ph): on X_k[ph], stage k-1's column ph
             const double nb = cH6 * w[0];                // H6(k, ph): on X_k[ph+6] (ph < 6)
-            // stage 0 zeroes the last stage's na / nb (that stage has no next stage)
+            // stage 0 zeroes the last stage's na / nb (that stage has no next stage:
+            // its coefficients read zero)
             *(cl ? Wbo : Wdump) = bo;
-            *(cl ? Wna : Wdump) = hp ? na : 0.0;
-            *(cl ? Wnb : Wdump) = hp && !isv ? nb : 0.0;
+            *(cl ? Wna : Wdump) = na;
+            *(cl ? Wnb : Wdump) = nb;
           }
           sync_all();
           STAMP(3);
@@ -1408,14 +1419,12 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           sX = XSr[oXS];
           double fwl[6], qll[6];
 #pragma unroll
-          for (int i = 0; i < 6; ++i) { fwl[i] = FWr[oFW + i]; qll[i] = QLr[oQL + i]; }
-          const double eXd = Ab[oXd], eHd = Ab[oHd], eH6 = Ab[oH6];
+          for (int i = 0; i < 6; ++i) { fwl[i] = FWr[oFW + i]; qll[i] = QLr[oQLm + i]; }
+          const double eXd = Ab[oXd], eHd = Ab[oHdm], eH6 = Ab[oH6m];
           const double cFb = Ab[oFb], cFa = Ab[oFa], cF4 = Ab[oF4], cSw = Ab[oF + 4];
           asm volatile("" : : : "memory");
           {
-            const double g0 = eXd * sX;
-            const double g1 = g0 + eHd * xa;
-            gv = hp ? g1 : g0;  // used from the lanes of rows 6..11 only
+            gv = eXd * sX + eHd * xa;  // used from the lanes of rows 6..11 only
             sf = uf - bdot_ln6v(fwl, gv, 0.0);
           }
           STAMP(9);
@@ -1424,12 +1433,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           {
             double ax[3];
             {
-              double dyn = eXd * sX;
-              const double d1 = dyn + eHd * xa;
-              const double d2 = d1 + eH6 * xb;
-              dyn = hp ? (isv ? d1 : d2) : dyn;
+              // B f on the velocity rows (zero coefficients elsewhere)
               const double bfv = beta * ri[0] - bdot_ln6v(qll, gv, 0.0);
-              dyn = isv ? dyn + bfv : dyn;
+              const double dyn = (gv + eH6 * xb) + bfv;
               // friction rows: lane c < 3 owns row c, lane 3 rows 3 and 4 (all loads unconditional)
               const double q0 = qbc<0>(sf), q1 = qbc<1>(sf), q2 = qbc<2>(sf);
               const double frA = cFb * q2 + cFa * (ta0 ? q0 : q1);
@@ -1443,7 +1449,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             for (int j = 0; j < 3; ++j) {
               const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
               const double tt = zr + ri[j] * y[j];
-              const double zn = tt < lo[j] ? lo[j] : (tt > hi[j] ? hi[j] : tt);
+              const double zn = fmin(fmax(tt, lo[j]), hi[j]);  // osqp project: c_min(c_max(tt, l), u)
               y[j] = y[j] + rr[j] * (zr - zn);
               z[j] = zn;
             }

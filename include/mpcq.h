@@ -152,6 +152,65 @@ int mpcq_solve_batch(mpcq_ctx* ctx, int64_t batch, const double* xref,
                      const double* warm_y, double* f0, double* x, double* y,
                      int32_t* status, int32_t* iters, int32_t* info, uint32_t flags);
 
+/* ---- footstep planner ------------------------------------------------------
+ * The producer of (xref, fsteps): FootstepPlanner.py.  Per instance the
+ * planner keeps the reference object's mutable state — the gait table
+ * gait [20][5] (durations + contact bits, FootstepPlanner.py:58-62,193-213),
+ * the rotation-command state machine (flag_rotation_command,
+ * h_rotation_command, FootstepPlanner.py:67-68,130-154) and xref itself
+ * (getRefStates only rewrites some rows in some states, so xref is in/out).
+ *
+ * Parameters (mpcq_default_planner_params): FootstepPlanner.py:18-52,321,352. */
+typedef struct mpcq_planner_params {
+  double dt;            /* MPC time step, 0.02 */
+  double T_gait;        /* 0.32 (FootstepPlanner.py:51); getRefStates' linspace end points */
+  double h_ref;         /* 0.2027682 (processing.py:131 passes it to getRefStates) */
+  double k_feedback;    /* 0.03 */
+  double L;             /* 0.12: bound on the (x, y) deviation from the shoulders */
+  double g;             /* 9.81 */
+  double t_stance;      /* 0.16 (compute_next_footstep) */
+  double cmd_threshold; /* 0.05: joystick dead band of the height command */
+  double shoulders[8];  /* row-major 2x4: x of FL FR HL HR, then y */
+  double reduced_offset[8]; /* row-major 2x4 subtracted when reduced (FootstepPlanner.py:320-322) */
+  int32_t reserved[8];
+} mpcq_planner_params;
+
+/* operations of mpcq_plan_batch, applied in this order */
+#define MPCQ_PLAN_ROLL 1u       /* FootstepPlanner.roll (FootstepPlanner.py:401-425) */
+#define MPCQ_PLAN_FOOTSTEPS 2u  /* compute_footsteps (FootstepPlanner.py:284-361) */
+#define MPCQ_PLAN_REFSTATES 4u  /* getRefStates (FootstepPlanner.py:76-159) */
+/* update_fsteps(k > 0) + getRefStates: the once-per-tick sequence of processing.py:81-131 */
+#define MPCQ_PLAN_TICK (MPCQ_PLAN_ROLL | MPCQ_PLAN_FOOTSTEPS | MPCQ_PLAN_REFSTATES)
+
+void mpcq_default_planner_params(mpcq_planner_params* pp);
+
+/*
+ * Replaces FootstepPlanner.update_fsteps(k, l_feet, v_cur, v_ref, h, oMl, _, reduced)
+ * (FootstepPlanner.py:427-459, minus its viewer code) and getRefStates(k, T_gait,
+ * lC, abg, lV, lW, v_ref, h_ref) (FootstepPlanner.py:76-159) for a batch.
+ *   ops       MPCQ_PLAN_* bits
+ *   k         getRefStates' k (only k == 0 is distinguished, FootstepPlanner.py:105)
+ *   state     [B][12] lC, abg, lV, lW (local frame)             REFSTATES
+ *   v_cur     [B][6]  compute_footsteps' v_cur; NULL = state[6:12] (processing.py:81)
+ *   h         [B]     compute_footsteps' h;    NULL = state[2]   (processing.py:82)
+ *   l_feet    [B][3][4] feet positions, local frame                FOOTSTEPS
+ *   v_ref     [B][6]
+ *   reduced   [B] int32, NULL = 0
+ *   gait      [B][20][5]  in/out
+ *   rot_flag  [B] int32 in/out, h_rot [B] in/out   (REFSTATES; 0 / 0.2 initially)
+ *   xref      [B][12][N+1] in/out                                  REFSTATES
+ *   fsteps    [B][20][13] out                                      FOOTSTEPS
+ *   status    [B] out (optional): 0, or MPCQ_STATUS_BAD_GAIT where the reference
+ *             raises (gait table without a zero-duration terminator / empty); the
+ *             instance's buffers are then left unchanged.  Otherwise the table
+ *             is followed exactly as the reference indexes it (an empty first row
+ *             makes roll() look at row -1 = row 19, as Python does). */
+int mpcq_plan_batch(mpcq_ctx* ctx, const mpcq_planner_params* pp, int64_t batch, uint32_t ops,
+                    int k, const double* state, const double* v_cur, const double* h,
+                    const double* l_feet, const double* v_ref, const int32_t* reduced,
+                    double* gait, int32_t* rot_flag, double* h_rot, double* xref, double* fsteps,
+                    int32_t* status, uint32_t flags);
+
 /* ---- diagnostics -----------------------------------------------------------
  * Device buffer [B][16] (uint64) that a diagnostic build of the library
  * (compiled with -DMPCQ_STAMPS, libmpcq_stamps.so) fills with per-phase

@@ -398,6 +398,84 @@ int mpcq_solve_batch(mpcq_ctx* c, int64_t B, const double* xref, const double* f
                       nullptr, f0, x, y, status, iters, nullptr, info, flags);
 }
 
+// FootstepPlanner constants (FootstepPlanner.py:18-52, 316-322, 376; processing.py:131).
+void mpcq_default_planner_params(mpcq_planner_params* pp) {
+  if (!pp) return;
+  memset(pp, 0, sizeof(*pp));
+  pp->dt = 0.02;
+  pp->T_gait = 0.32;
+  pp->h_ref = 0.2027682;
+  pp->k_feedback = 0.03;
+  pp->L = 0.12;
+  pp->g = 9.81;
+  pp->t_stance = 0.16;
+  pp->cmd_threshold = 0.05;
+  const double sh[8] = {0.19, 0.19, -0.19, -0.19, 0.15005, -0.15005, 0.15005, -0.15005};
+  memcpy(pp->shoulders, sh, sizeof(sh));
+  const double ro[8] = {0.14, 0.14, -0.14, -0.14, 0.12, -0.12, 0.12, -0.12};
+  memcpy(pp->reduced_offset, ro, sizeof(ro));
+}
+
+int mpcq_plan_batch(mpcq_ctx* c, const mpcq_planner_params* pp, int64_t B, uint32_t ops, int k,
+                    const double* state, const double* v_cur, const double* h, const double* l_feet,
+                    const double* v_ref, const int32_t* reduced, double* gait, int32_t* rot_flag,
+                    double* h_rot, double* xref, double* fsteps, int32_t* status, uint32_t flags) {
+  int rc = check_ctx(c, B);
+  if (rc) return rc;
+  if (ops == 0 || (ops & ~(uint32_t)MPCQ_PLAN_TICK)) return fail(MPCQ_E_INVALID, "ops must be MPCQ_PLAN_* bits");
+  if (!gait || !v_ref || !state) return fail(MPCQ_E_INVALID, "gait, state and v_ref are required");
+  if ((ops & MPCQ_PLAN_FOOTSTEPS) && (!l_feet || !fsteps))
+    return fail(MPCQ_E_INVALID, "MPCQ_PLAN_FOOTSTEPS needs l_feet and fsteps");
+  if ((ops & MPCQ_PLAN_REFSTATES) && (!rot_flag || !h_rot || !xref))
+    return fail(MPCQ_E_INVALID, "MPCQ_PLAN_REFSTATES needs rot_flag, h_rot and xref");
+  mpcq_planner_params P;
+  if (pp) P = *pp;
+  else mpcq_default_planner_params(&P);
+  if (!(P.dt > 0) || !(P.g > 0) || !(P.T_gait > P.dt)) return fail(MPCQ_E_INVALID, "planner needs dt > 0, g > 0, T_gait > dt");
+  if (B == 0) return MPCQ_OK;
+  DeviceGuard g(c->device);
+  const int N = c->N;
+  const size_t n12 = 12 * (N + 1);
+  mpcq::PlanArgs a{};
+  a.batch = B;
+  a.N = N;
+  a.ops = ops;
+  a.k = k;
+  const bool dev = flags & MPCQ_FLAG_DEVICE_PTRS;
+  const bool fo = ops & MPCQ_PLAN_FOOTSTEPS, rs = ops & MPCQ_PLAN_REFSTATES;
+  enum { ST, VC, H, LF, VR, RD, GA, RF, HR, XR, FS, SS, NX };
+  // in/out buffers are staged both ways (host_in and host_out both set)
+  Xfer xs[NX] = {{state, nullptr, (size_t)B * 96, nullptr},
+                 {v_cur, nullptr, (size_t)B * 48, nullptr},
+                 {h, nullptr, (size_t)B * 8, nullptr},
+                 {fo ? l_feet : nullptr, nullptr, (size_t)B * 96, nullptr},
+                 {v_ref, nullptr, (size_t)B * 48, nullptr},
+                 {reduced, nullptr, (size_t)B * 4, nullptr},
+                 {gait, gait, (size_t)B * 800, nullptr},
+                 {rs ? rot_flag : nullptr, rs ? rot_flag : nullptr, (size_t)B * 4, nullptr},
+                 {rs ? h_rot : nullptr, rs ? h_rot : nullptr, (size_t)B * 8, nullptr},
+                 {rs ? xref : nullptr, rs ? xref : nullptr, B * n12 * 8, nullptr},
+                 // fsteps: staged in as well so a BAD_GAIT instance keeps the caller's values
+                 {fo ? fsteps : nullptr, fo ? fsteps : nullptr, (size_t)B * 260 * 8, nullptr},
+                 {nullptr, status, (size_t)B * 4, nullptr}};
+  if (!dev) {
+    rc = stage(c, xs, NX);
+    if (rc) return rc;
+    a.state = (const double*)xs[ST].dev; a.v_cur = (const double*)xs[VC].dev; a.h = (const double*)xs[H].dev;
+    a.l_feet = (const double*)xs[LF].dev; a.v_ref = (const double*)xs[VR].dev;
+    a.reduced = (const int32_t*)xs[RD].dev; a.gait = (double*)xs[GA].dev; a.rot_flag = (int32_t*)xs[RF].dev;
+    a.h_rot = (double*)xs[HR].dev; a.xref = (double*)xs[XR].dev; a.fsteps = (double*)xs[FS].dev;
+    a.status = (int32_t*)xs[SS].dev;
+  } else {
+    a.state = state; a.v_cur = v_cur; a.h = h; a.l_feet = l_feet; a.v_ref = v_ref; a.reduced = reduced;
+    a.gait = gait; a.rot_flag = rot_flag; a.h_rot = h_rot; a.xref = xref; a.fsteps = fsteps; a.status = status;
+  }
+  HIP_TRY(mpcq::launch_plan(P, a, c->stream));
+  if (!dev) return unstage(c, xs, NX);
+  if (!(flags & MPCQ_FLAG_ASYNC)) HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPCQ_OK;
+}
+
 int mpcq_debug_set_stamps(mpcq_ctx* c, void* buf) {
   if (!c) return fail(MPCQ_E_INVALID, "ctx is NULL");
   c->stamps = (uint64_t*)buf;

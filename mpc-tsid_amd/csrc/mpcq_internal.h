@@ -33,7 +33,29 @@ struct LaunchArgs {
   uint64_t* stamps;    // [B][16] diagnostic build only (MPCQ_STAMPS): cycles per phase
 };
 
-// Launchers (mpcq_kernels.hip).  Return hipError_t.
+// Planner launch (mpcq_planner.hip); layouts in include/mpcq.h (mpcq_plan_batch).
+struct PlanArgs {
+  int64_t batch;
+  int N;
+  unsigned ops;        // MPCQ_PLAN_* bits
+  int k;
+  const double* state; // [B][12]
+  const double* v_cur; // [B][6] or null (state[6:12])
+  const double* h;     // [B] or null (state[2])
+  const double* l_feet;// [B][3][4]
+  const double* v_ref; // [B][6]
+  const int32_t* reduced; // [B] or null
+  double* gait;        // [B][20][5] in/out
+  int32_t* rot_flag;   // [B] in/out
+  double* h_rot;       // [B] in/out
+  double* xref;        // [B][12][N+1] in/out
+  double* fsteps;      // [B][20][13] out
+  int32_t* status;     // [B] or null
+};
+
+hipError_t launch_plan(const mpcq_planner_params& pp, const PlanArgs& a, hipStream_t s);
+
+// Launchers (mpcq_engine.hip).  Return hipError_t.
 hipError_t launch_formulate(int N, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);
 hipError_t launch_solve(int N, bool fused, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);
 bool horizon_supported(int N);

@@ -1,0 +1,260 @@
+// mpcq_planner.hip — batched FootstepPlanner for MI355X (gfx950): the producer
+// of the engine's inputs (xref, fsteps), FootstepPlanner.py:76-425.
+//
+// One wave64 per instance.  The per-instance state (gait table, xref, the
+// rotation-command state machine) is read once, updated on chip and written
+// once; every HBM row is moved by consecutive lanes.
+//   roll               FootstepPlanner.py:401-425   lane-parallel row shift in LDS
+//   compute_footsteps  FootstepPlanner.py:284-361   lane c < 12 walks column c of
+//                                                   fsteps over the phases
+//   getRefStates       FootstepPlanner.py:76-159    lane j <= N owns xref column j
+//
+// Rounding follows numpy's evaluation order exactly (the oracle
+// oracle/planner_oracle.c does the same and matches the reference bit for
+// bit): no contraction of a*b+c into FMAs, except inside np.dot(R,
+// next_footstep) whose BLAS kernel does use FMAs; cumsum left to right.
+// Only cos/sin can differ (ocml vs the host libm) by an ulp.
+#include <math.h>
+
+#include "mpcq_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace mpcq {
+namespace {
+
+struct PlanShared {
+  double gait[100];
+  double fs[260];
+  double v6[33], v7[33];
+  int bad;
+};
+
+// numpy.linspace(a, b, n)[i] with endpoint: i * ((b - a) / (n - 1)) + a, last = b
+__device__ __forceinline__ double linspace_at(double a, double b, int n, int i) {
+  if (i == n - 1) return b;
+  const double step = (b - a) / (double)(n - 1);
+  return (double)i * step + a;
+}
+
+__global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, PlanArgs a) {
+  __shared__ PlanShared sh;
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  if (b >= a.batch) return;
+  const int N = a.N, NP = a.N + 1;
+  double* gg = a.gait + b * 100;
+  const double* st = a.state + b * 12;
+  const double* vr = a.v_ref + b * 6;
+
+  for (int e = lane; e < 100; e += 64) sh.gait[e] = gg[e];
+  if (lane == 0) sh.bad = 0;
+  __syncthreads();
+
+  // ---- roll (FootstepPlanner.py:401-425)
+  if (a.ops & MPCQ_PLAN_ROLL) {
+    const bool z = lane < 20 && sh.gait[5 * lane] == 0.0;
+    const uint64_t zm = __ballot(z);
+    if (zm == 0) {
+      if (lane == 0) sh.bad = 1;  // next(..., 0.0)[0] raises
+    } else {
+      const int index = __ffsll((unsigned long long)zm) - 1;
+      const int last = (index + 19) % 20;  // gait[index - 1]; Python wraps -1
+      bool same = true;
+#pragma unroll
+      for (int q = 1; q < 5; ++q) same = same && (sh.gait[q] == sh.gait[5 * last + q]);
+      __syncthreads();
+      if (lane == 0) {
+        if (same) {
+          sh.gait[5 * last] += 1.0;
+        } else {
+          for (int q = 1; q < 5; ++q) sh.gait[5 * index + q] = sh.gait[q];
+          sh.gait[5 * index] = 1.0;
+        }
+      }
+      __syncthreads();
+      if (!(sh.gait[0] > 1.0)) {  // the current phase ends: shift the rows up
+        // np.roll(gait, -1, axis=0) then a zero last row: element e <- e + 5
+        const double t0 = sh.gait[lane + 5];
+        const double t1 = lane + 69 < 100 ? sh.gait[lane + 69] : 0.0;
+        __syncthreads();
+        sh.gait[lane] = t0;
+        if (lane + 64 < 100) sh.gait[lane + 64] = t1;  // lanes 31..35: row 19 = 0
+      } else {
+        __syncthreads();
+        if (lane == 0) sh.gait[0] -= 1.0;
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  // ---- validity of compute_footsteps' walk: a terminator among rows 1..19
+  if (a.ops & MPCQ_PLAN_FOOTSTEPS) {
+    const bool z = lane >= 1 && lane < 20 && !(sh.gait[5 * lane] != 0.0);
+    if (__ballot(z) == 0 && lane == 0) sh.bad = 1;  // self.gait[20, 0]: IndexError
+  }
+  __syncthreads();
+  if (sh.bad) {
+    if (lane == 0 && a.status) a.status[b] = MPCQ_STATUS_BAD_GAIT;
+    return;  // the instance's buffers stay as they were (the reference raised)
+  }
+  if (a.ops & MPCQ_PLAN_ROLL)
+    for (int e = lane; e < 100; e += 64) gg[e] = sh.gait[e];
+
+  // ---- compute_footsteps (FootstepPlanner.py:284-361)
+  if (a.ops & MPCQ_PLAN_FOOTSTEPS) {
+    const double* vc = a.v_cur ? a.v_cur + b * 6 : st + 6;
+    const double h = a.h ? a.h[b] : st[2];
+    const int reduced = a.reduced ? a.reduced[b] : 0;
+    for (int e = lane; e < 260; e += 64) sh.fs[e] = (e % 13 == 0) ? sh.gait[5 * (e / 13)] : NAN;
+    __syncthreads();
+    if (lane < 12) {
+      const int c = lane, q = c / 3, r = c % 3;
+      // next_footstep rows 0..1 of foot q: compute_next_footstep(v_ref, v_ref, h)
+      // (FootstepPlanner.py:316, 363-399); row 2 is 0
+      double nf[2];
+      {
+        const double cr0 = vr[1] * vr[5] - vr[2] * vr[4];  // np.cross(v_ref[0:3], v_ref[3:6])
+        const double cr1 = vr[2] * vr[3] - vr[0] * vr[5];
+        const double coef = 0.5 * sqrt(h / pp.g);
+        const double half = pp.t_stance * 0.5;
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+          double v = 0.0 + half * vr[rr];
+          v = v + pp.k_feedback * (vr[rr] - vr[rr]);
+          v = v + coef * (rr == 0 ? cr0 : cr1);
+          if (v > pp.L) v = pp.L;
+          if (v < -pp.L) v = -pp.L;
+          v = v + pp.shoulders[4 * rr + q];
+          if (reduced) v = v - pp.reduced_offset[4 * rr + q];
+          nf[rr] = v;
+        }
+      }
+      // row 0: stance feet where they are (l_feet.ravel('F')[c] = l_feet[r][q])
+      const double l0 = sh.gait[1 + q] == 1.0 ? a.l_feet[b * 12 + 4 * r + q] : NAN;
+      double prev = l0;  // fsteps[i-1, 1+c]
+      sh.fs[1 + c] = l0;
+      bool prev_st = sh.gait[1 + q] == 1.0;
+      double dt_cum = 0.0;
+      for (int i = 1; i < 20; ++i) {
+        const double d = sh.gait[5 * i];
+        if (!(d != 0.0)) break;
+        dt_cum += sh.gait[5 * (i - 1)] * pp.dt;
+        const bool cur_st = sh.gait[5 * i + 1 + q] == 1.0;
+        double v = NAN;
+        if (prev_st && cur_st) {
+          v = prev;
+        } else if (!prev_st && cur_st) {
+          const double angle = vr[5] * dt_cum;
+          const double co = cos(angle), si = sin(angle);
+          double dx, dy;
+          if (vr[5] != 0.0) {
+            dx = (vc[0] * si + vc[1] * (co - 1.0)) / vr[5];
+            dy = (vc[1] * si - vc[0] * (co - 1.0)) / vr[5];
+          } else {
+            dx = vc[0] * dt_cum;
+            dy = vc[1] * dt_cum;
+          }
+          // (R @ next_footstep)[r, q] + d[r]; R = [[c, -s, 0], [s, c, 0], [0, 0, 1]]
+          const double R0 = r == 0 ? co : (r == 1 ? si : 0.0);
+          const double R1 = r == 0 ? -si : (r == 1 ? co : 0.0);
+          const double R2 = r == 2 ? 1.0 : 0.0;
+          double w = R0 * nf[0];
+          w = fma(R1, nf[1], w);
+          w = fma(R2, 0.0, w);
+          v = w + (r == 0 ? dx : (r == 1 ? dy : 0.0));
+        }
+        sh.fs[13 * i + 1 + c] = v;
+        prev = v;
+        prev_st = cur_st;
+      }
+    }
+    __syncthreads();
+    double* gf = a.fsteps + b * 260;
+    for (int e = lane; e < 260; e += 64) gf[e] = sh.fs[e];
+  }
+
+  // ---- getRefStates (FootstepPlanner.py:76-159)
+  if (a.ops & MPCQ_PLAN_REFSTATES) {
+    double* gx = a.xref + b * 12 * NP;
+    const int j = lane;
+    const bool col = j < NP;
+    double x[12];
+#pragma unroll
+    for (int r = 0; r < 12; ++r) x[r] = col ? gx[r * NP + j] : 0.0;
+    const double Tg = pp.T_gait, dt = pp.dt;
+    if (col && j >= 1) {
+      const double yaw = linspace_at(0.0, Tg - dt, N, j - 1) * vr[5];
+      const double c = cos(yaw), s = sin(yaw);
+      x[6] = vr[0] * c - vr[1] * s;
+      x[7] = vr[0] * s + vr[1] * c;
+      sh.v6[j] = x[6];
+      sh.v7[j] = x[7];
+    }
+    __syncthreads();
+    if (col && j >= 1) {
+      double a0 = 0.0, a1 = 0.0;  // np.cumsum: left to right
+      for (int i = 1; i <= j; ++i) {
+        a0 += sh.v6[i];
+        a1 += sh.v7[i];
+      }
+      x[0] = dt * a0 + st[0];
+      x[1] = dt * a1 + st[1];
+      if (a.k == 0) x[2] = pp.h_ref;
+      x[5] = vr[5] * linspace_at(dt, Tg, N, j - 1);
+      x[11] = vr[5];
+    }
+    if (j == 0) {
+#pragma unroll
+      for (int r = 0; r < 12; ++r) x[r] = st[r];
+    }
+    // height / rotation command state machine (uniform per instance)
+    int flag = a.rot_flag[b];
+    double h_rot = a.h_rot[b];
+    const double step = pp.cmd_threshold;
+    const double v2 = vr[2];
+    if (fabs(v2) > step && flag != 1) flag = 1;
+    int branch = 0;
+    if (fabs(v2) > step && flag == 1) {
+      h_rot += v2 * dt;
+      branch = 1;
+    } else if (fabs(v2) < step && flag == 1) {
+      flag = 2;
+      branch = 2;
+    } else if (flag == 0) {
+      branch = 3;
+    }
+    if (col && j >= 1) {
+      if (branch == 1) { x[2] = h_rot; x[8] = v2; }
+      else if (branch == 2) { x[8] = 0.0; x[9] = 0.0; x[10] = 0.0; }
+      else if (branch == 3) { x[2] = pp.h_ref; x[8] = 0.0; }
+      if (flag != 0) {
+        const double to = linspace_at(0.0, Tg - dt, N, j - 1);
+        x[3] = st[3] + vr[3] * to;  // xref[3, 0] was just set to abg[0]
+        x[4] = st[4] + vr[4] * to;
+        x[9] = vr[3];
+        x[10] = vr[4];
+      }
+    }
+    if (col) {
+#pragma unroll
+      for (int r = 0; r < 12; ++r) gx[r * NP + j] = x[r];
+    }
+    if (lane == 0) {
+      a.rot_flag[b] = flag;
+      a.h_rot[b] = h_rot;
+    }
+  }
+  if (lane == 0 && a.status) a.status[b] = 0;
+}
+
+}  // namespace
+
+hipError_t launch_plan(const mpcq_planner_params& pp, const PlanArgs& a, hipStream_t s) {
+  if (a.batch <= 0) return hipSuccess;
+  if (a.N + 1 > 64 || a.N + 1 > 33) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(planner_kernel, dim3((unsigned)a.batch), dim3(64), 0, s, pp, a);
+  return hipGetLastError();
+}
+
+}  // namespace mpcq

@@ -5,11 +5,13 @@ Public surface:
   Engine            batched formulate / qp_solve / solve over libmpcq.so
   default_params    reference constants + OSQP 0.6 settings (MPC.py:25-39, 414-416)
   pattern, dims     CSC pattern / sizes of MPC.create_ML
+  Engine.plan       batched FootstepPlanner (roll / compute_footsteps / getRefStates)
   synth             seeded synthetic inputs shaped like FootstepPlanner's
 """
 from . import synth  # noqa: F401
 from ._lib import (FLAG_ASYNC, FLAG_DEVICE_PTRS, MODE_SETUP, MODE_UPDATE,  # noqa: F401
-                   STATUS_BAD_GAIT, STATUS_FACTOR_FAILED, STATUS_MAX_ITER_REACHED,
+                   PLAN_FOOTSTEPS, PLAN_REFSTATES, PLAN_ROLL, PLAN_TICK, PlannerParams,
+                   default_planner_params, STATUS_BAD_GAIT, STATUS_FACTOR_FAILED, STATUS_MAX_ITER_REACHED,
                    STATUS_NONFINITE, STATUS_SOLVED, STATUS_SOLVED_INACCURATE, MpcqError,
                    Params, build, default_params, lib, supported_horizons)
 from .engine import Engine, dims, pattern  # noqa: F401

@@ -30,11 +30,14 @@ FLAG_DEVICE_PTRS = 1
 FLAG_ASYNC = 2
 MODE_UPDATE = 0
 MODE_SETUP = 1
+PLAN_ROLL, PLAN_FOOTSTEPS, PLAN_REFSTATES = 1, 2, 4
+PLAN_TICK = PLAN_ROLL | PLAN_FOOTSTEPS | PLAN_REFSTATES
 
 EXPORTS = ("mpcq_abi_version", "mpcq_default_params", "mpcq_dims", "mpcq_pattern",
            "mpcq_supported_horizons", "mpcq_last_error", "mpcq_create", "mpcq_destroy",
            "mpcq_set_stream", "mpcq_last_kernel_ms", "mpcq_formulate_batch",
-           "mpcq_qp_solve_batch", "mpcq_solve_batch", "mpcq_debug_set_stamps")
+           "mpcq_qp_solve_batch", "mpcq_solve_batch", "mpcq_default_planner_params",
+           "mpcq_plan_batch", "mpcq_debug_set_stamps")
 
 
 class MpcqError(RuntimeError):
@@ -82,6 +85,24 @@ class Params(C.Structure):
         return out
 
 
+class PlannerParams(C.Structure):
+    """struct mpcq_planner_params (include/mpcq.h)."""
+
+    _fields_ = [
+        ("dt", C.c_double),
+        ("T_gait", C.c_double),
+        ("h_ref", C.c_double),
+        ("k_feedback", C.c_double),
+        ("L", C.c_double),
+        ("g", C.c_double),
+        ("t_stance", C.c_double),
+        ("cmd_threshold", C.c_double),
+        ("shoulders", C.c_double * 8),
+        ("reduced_offset", C.c_double * 8),
+        ("reserved", C.c_int32 * 8),
+    ]
+
+
 def build(force: bool = False) -> str:
     """Compile libmpcq.so for gfx950 with hipcc (csrc/Makefile)."""
     if force or not os.path.exists(LIB_PATH):
@@ -118,9 +139,13 @@ def lib():
     L.mpcq_solve_batch.argtypes = [vp, C.c_int64, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp,
                                    C.c_uint32]
     L.mpcq_debug_set_stamps.argtypes = [vp, vp]
+    L.mpcq_default_planner_params.argtypes = [C.POINTER(PlannerParams)]
+    L.mpcq_default_planner_params.restype = None
+    L.mpcq_plan_batch.argtypes = [vp, C.POINTER(PlannerParams), C.c_int64, C.c_uint32, C.c_int] + [vp] * 12 + [C.c_uint32]
     for name in ("mpcq_dims", "mpcq_pattern", "mpcq_supported_horizons", "mpcq_create",
                  "mpcq_destroy", "mpcq_set_stream", "mpcq_last_kernel_ms", "mpcq_formulate_batch",
-                 "mpcq_qp_solve_batch", "mpcq_solve_batch", "mpcq_debug_set_stamps"):
+                 "mpcq_qp_solve_batch", "mpcq_solve_batch", "mpcq_default_planner_params",
+           "mpcq_plan_batch", "mpcq_debug_set_stamps"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L
@@ -139,6 +164,16 @@ def default_params(**overrides) -> Params:
     for k, v in overrides.items():
         if not hasattr(p, k):
             raise AttributeError(f"unknown parameter {k}")
+        setattr(p, k, v)
+    return p
+
+
+def default_planner_params(**overrides) -> PlannerParams:
+    p = PlannerParams()
+    lib().mpcq_default_planner_params(C.byref(p))
+    for k, v in overrides.items():
+        if not hasattr(p, k):
+            raise AttributeError(f"unknown planner parameter {k}")
         setattr(p, k, v)
     return p
 

@@ -138,6 +138,48 @@ class Engine:
                                          _p(x), _p(y), _p(st), _p(it), _p(info), 0))
         return dict(f0=f0, x=x, y=y, status=st, iters=it, rho_updates=info[:, 0], polish=info[:, 1])
 
+    # ------------------------------------------------------------------ footstep planner
+    def plan(self, ops: int, k: int, state, l_feet, v_ref, gait, rot_flag, h_rot, xref, fsteps,
+             reduced=None, v_cur=None, h=None, params: L.PlannerParams | None = None):
+        """FootstepPlanner.update_fsteps + getRefStates for a batch (mpcq_plan_batch).
+
+        ``gait`` (B,20,5), ``rot_flag`` (B,) int32, ``h_rot`` (B,), ``xref`` (B,12,N+1) and
+        ``fsteps`` (B,20,13) are C-contiguous arrays updated in place.  Returns status (B,):
+        0, or STATUS_BAD_GAIT where the reference raises (that instance left unchanged)."""
+        B = int(np.shape(state)[0])
+        N = self.n_steps
+        state = _f64(state, (B, 12))
+        v_ref = _f64(v_ref, (B, 6))
+        l_feet = None if l_feet is None else _f64(l_feet, (B, 3, 4))
+        v_cur = None if v_cur is None else _f64(v_cur, (B, 6))
+        h = None if h is None else _f64(h, (B,))
+        red = None if reduced is None else np.ascontiguousarray(np.broadcast_to(np.asarray(reduced, np.int32), (B,)))
+        for name, arr, shp, dt in (("gait", gait, (B, 20, 5), np.float64), ("rot_flag", rot_flag, (B,), np.int32),
+                                   ("h_rot", h_rot, (B,), np.float64), ("xref", xref, (B, 12, N + 1), np.float64),
+                                   ("fsteps", fsteps, (B, 20, 13), np.float64)):
+            if arr is None:
+                continue
+            if arr.shape != shp or arr.dtype != dt or not arr.flags.c_contiguous:
+                raise ValueError(f"{name} must be a C-contiguous {np.dtype(dt).name} array of shape {shp}")
+        st = np.empty(B, np.int32)
+        pp = params if params is not None else L.default_planner_params(dt=self.params.dt)
+        L.check(L.lib().mpcq_plan_batch(self._h, C.byref(pp), B, ops, int(k), _p(state), _p(v_cur), _p(h),
+                                        _p(l_feet), _p(v_ref), _p(red), _p(gait), _p(rot_flag), _p(h_rot),
+                                        _p(xref), _p(fsteps), _p(st), 0))
+        return st
+
+    def plan_device(self, batch: int, ops: int, k: int, state_ptr: int, l_feet_ptr: int, v_ref_ptr: int,
+                    gait_ptr: int, rot_flag_ptr: int, h_rot_ptr: int, xref_ptr: int, fsteps_ptr: int,
+                    status_ptr: int = 0, reduced_ptr: int = 0, v_cur_ptr: int = 0, h_ptr: int = 0,
+                    params: L.PlannerParams | None = None, asynchronous: bool = False):
+        flags = L.FLAG_DEVICE_PTRS | (L.FLAG_ASYNC if asynchronous else 0)
+        v = lambda q: C.c_void_p(q) if q else None  # noqa: E731
+        pp = params if params is not None else L.default_planner_params(dt=self.params.dt)
+        L.check(L.lib().mpcq_plan_batch(self._h, C.byref(pp), int(batch), ops, int(k), v(state_ptr), v(v_cur_ptr),
+                                        v(h_ptr), v(l_feet_ptr), v(v_ref_ptr), v(reduced_ptr), v(gait_ptr),
+                                        v(rot_flag_ptr), v(h_rot_ptr), v(xref_ptr), v(fsteps_ptr), v(status_ptr),
+                                        flags))
+
     # ------------------------------------------------------------------ device pointers
     def set_stream(self, stream_handle: int | None):
         L.check(L.lib().mpcq_set_stream(self._h, C.c_void_p(stream_handle or 0)))

@@ -5,8 +5,10 @@ cpu_baseline leg of bench.py, always as the checker; the product package
 (mpc-tsid_amd/) never imports it.
 
 The restatement follows the reference MPC.py formulation (MPC.py:98-378,
-611-652) and the OSQP 0.6 ADMM that MPC.py:413-428 calls; see the C file's
-header for the exact list and DESIGN.md for how it is pinned.
+611-652) and the OSQP 0.6 ADMM that MPC.py:413-428 calls (mpcq_oracle.c), and
+the FootstepPlanner that produces MPC.run's inputs (FootstepPlanner.py:76-425,
+planner_oracle.c); see the C files' headers for the exact list and DESIGN.md
+for how each is pinned.
 """
 from __future__ import annotations
 
@@ -52,6 +54,24 @@ class Params(C.Structure):
     ]
 
 
+class PlannerParams(C.Structure):
+    """Mirror of struct mpcq_planner_params (include/mpcq.h)."""
+
+    _fields_ = [
+        ("dt", C.c_double),
+        ("T_gait", C.c_double),
+        ("h_ref", C.c_double),
+        ("k_feedback", C.c_double),
+        ("L", C.c_double),
+        ("g", C.c_double),
+        ("t_stance", C.c_double),
+        ("cmd_threshold", C.c_double),
+        ("shoulders", C.c_double * 8),
+        ("reduced_offset", C.c_double * 8),
+        ("reserved", C.c_int32 * 8),
+    ]
+
+
 def build(force: bool = False) -> str:
     """Compile liboracle.so with the Makefile next to this file."""
     if force or not os.path.exists(_LIB_PATH):
@@ -77,6 +97,9 @@ def lib():
         L.oracle_solve_batch.argtypes = [C.POINTER(Params), C.c_int, C.c_int64, dp, dp, C.c_int,
                                          dp, dp, ip, ip, C.c_int]
         L.oracle_num_threads.restype = C.c_int
+        L.oracle_default_planner_params.argtypes = [C.POINTER(PlannerParams)]
+        L.oracle_plan.argtypes = [C.POINTER(PlannerParams), C.c_int, C.c_uint, C.c_int, dp, dp, dp, dp, dp,
+                                  C.c_int, dp, ip, dp, dp, dp]
         _lib = L
     return _lib
 
@@ -163,6 +186,43 @@ def solve_batch(xref, fsteps, mode: int = 0, params: Params | None = None, nthre
     lib().oracle_solve_batch(C.byref(p), N, B, _dp(xref), _dp(fsteps), mode, _dp(f0), _dp(x),
                              _ip(st), _ip(it), nthreads)
     return dict(f0=f0, x=x, status=st, iters=it)
+
+
+def default_planner_params(**overrides) -> PlannerParams:
+    p = PlannerParams()
+    lib().oracle_default_planner_params(C.byref(p))
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    return p
+
+
+class Planner:
+    """One FootstepPlanner instance (planner_oracle.c): the state the reference
+    object keeps between ticks (gait, rotation state machine, xref, fsteps)."""
+
+    def __init__(self, N: int, gait, params: PlannerParams | None = None):
+        self.N = int(N)
+        self.p = params or default_planner_params()
+        self.gait = np.ascontiguousarray(gait, np.float64).copy()
+        self.flag = np.zeros(1, np.int32)
+        self.h_rot = np.array([0.20])  # FootstepPlanner.py:68
+        self.xref = np.zeros((12, N + 1))
+        self.fsteps = np.full((20, 13), np.nan)
+
+    def plan(self, ops: int, k: int, state, l_feet, v_ref, reduced=False, v_cur=None, h=None) -> int:
+        """ops = MPCQ_PLAN_* bits; returns 0 or MPCQ_STATUS_BAD_GAIT (buffers unchanged)."""
+        st = np.ascontiguousarray(state, np.float64).ravel()
+        lf = np.ascontiguousarray(l_feet, np.float64).reshape(3, 4)
+        vr = np.ascontiguousarray(v_ref, np.float64).ravel()
+        vc = None if v_cur is None else np.ascontiguousarray(v_cur, np.float64).ravel()
+        hh = None if h is None else np.array([h], np.float64)
+        return int(lib().oracle_plan(C.byref(self.p), self.N, ops, int(k), _dp(st), _dp(vc), _dp(hh), _dp(lf),
+                                     _dp(vr), int(bool(reduced)), _dp(self.gait), _ip(self.flag),
+                                     _dp(self.h_rot), _dp(self.xref), _dp(self.fsteps)))
+
+
+PLAN_ROLL, PLAN_FOOTSTEPS, PLAN_REFSTATES = 1, 2, 4
+PLAN_TICK = 7
 
 
 def num_threads() -> int:

@@ -1,0 +1,69 @@
+"""CPU: the planner restatement (oracle/planner_oracle.c) against the fixtures
+captured from the unmodified reference FootstepPlanner.py
+(tests/golden/gen_planner_golden.py).  Expected: bit-identical gait tables,
+fsteps, xref and rotation state machine on every tick of every scenario."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "planner_golden.npz")
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return np.load(GOLD)
+
+
+def replay(G, N, s, check):
+    """Drive one scenario through the oracle as processing.py:81-131 drives the reference."""
+    pl = O.Planner(N, G[f"n{N}_gait0"][s])
+    for j in range(G[f"n{N}_state"].shape[1]):
+        a = dict(state=G[f"n{N}_state"][s, j], l_feet=G[f"n{N}_l_feet"][s, j],
+                 v_ref=G[f"n{N}_v_ref"][s, j], reduced=bool(G[f"n{N}_reduced"][s, j]))
+        if j == 0:
+            assert pl.plan(O.PLAN_FOOTSTEPS, 0, **a) == 0
+        assert pl.plan(O.PLAN_TICK, j, **a) == 0
+        check(pl, j)
+
+
+@pytest.mark.parametrize("N", [16, 32])
+def test_planner_oracle_bit_exact(gold, N):
+    G = gold
+    for s in range(G[f"n{N}_state"].shape[0]):
+        def check(pl, j):
+            ctx = (N, str(G[f"n{N}_kind"][s]), j)
+            assert np.array_equal(pl.gait, G[f"n{N}_gait"][s, j]), ctx
+            assert np.array_equal(pl.fsteps, G[f"n{N}_fsteps"][s, j], equal_nan=True), ctx
+            assert np.array_equal(pl.xref, G[f"n{N}_xref"][s, j]), ctx
+            assert pl.flag[0] == G[f"n{N}_flag"][s, j], ctx
+            assert pl.h_rot[0] == G[f"n{N}_h_rot"][s, j], ctx
+        replay(G, N, s, check)
+
+
+def test_planner_oracle_fixture_coverage(gold):
+    # the fixtures exercise every state of the rotation-command state machine
+    # and both dx/dy branches (v_ref[5] == 0 and != 0)
+    for N in (16, 32):
+        assert set(np.unique(gold[f"n{N}_flag"]).tolist()) == {0, 1, 2}
+        assert (gold[f"n{N}_v_ref"][..., 5] == 0).any() and (gold[f"n{N}_v_ref"][..., 5] != 0).any()
+        assert gold[f"n{N}_reduced"].any()
+
+
+def test_planner_oracle_bad_gait(gold):
+    # the reference raises on a table without a terminator (roll: TypeError,
+    # compute_footsteps: IndexError); the restatement reports BAD_GAIT and
+    # leaves the state alone
+    assert str(gold["bad_roll_raises"]) == "TypeError"
+    assert str(gold["bad_footsteps_raises"]) == "IndexError"
+    st = np.zeros(12); st[2] = 0.2
+    lf = np.zeros((3, 4)); v = np.zeros(6)
+    for ops in (O.PLAN_ROLL, O.PLAN_FOOTSTEPS, O.PLAN_TICK):
+        pl = O.Planner(16, gold["bad_gait"])
+        before = (pl.gait.copy(), pl.fsteps.copy(), pl.xref.copy())
+        assert pl.plan(ops, 1, st, lf, v) == -11
+        assert np.array_equal(pl.gait, before[0])
+        assert np.array_equal(pl.fsteps, before[1], equal_nan=True)
+        assert np.array_equal(pl.xref, before[2])

@@ -211,6 +211,67 @@ int mpcq_plan_batch(mpcq_ctx* ctx, const mpcq_planner_params* pp, int64_t batch,
                     double* gait, int32_t* rot_flag, double* h_rot, double* xref, double* fsteps,
                     int32_t* status, uint32_t flags);
 
+/* ---- closed-loop session ---------------------------------------------------
+ * B robots, each running the reference's once-per-tick MPC sequence
+ * (processing.py:81-131 + MPC.run, MPC.py:460-514) with every piece of state
+ * the reference keeps between ticks resident in HBM:
+ *   FootstepPlanner: gait table, rotation state machine, xref, fsteps;
+ *   MPC / osqp workspace: x (the next tick's warm start is x shifted by one
+ *   stage, MPC.py:403-406), y and rho (kept by osqp across solves), q_w.
+ * A tick is three launches on the context's stream, no host round trip:
+ *   planner (roll + compute_footsteps + getRefStates; at k == 0 the extra
+ *   compute_footsteps of processing.py:80-82 first) -> fused formulation + OSQP
+ *   solve (k == 0: create_matrices, cold start; k > 0: update_matrices, warm) ->
+ *   retrieve (f_applied, x_robot, q_next / v_next, q_w, the Logger's cost
+ *   components, the next warm start, the virtual robot's next state).
+ *
+ * Virtual robot (optional): passing state == NULL / l_feet == NULL to a tick
+ * takes the robot's state from the previous tick's prediction x_robot[:, 0],
+ * re-expressed in the new local frame (origin under the base, yaw removed,
+ * Interface.py:100-138), and the stance feet from the previous fsteps — the
+ * "MPC future state as the robot state" path of processing.py:33-38.  It makes
+ * a closed loop run entirely on the device (tests, benchmarks). */
+typedef struct mpcq_session mpcq_session;
+
+/* gait0 [B][20][5] (NULL: create_walking_trot for this ctx's horizon, FootstepPlanner.py:193-214).
+ * pp NULL = mpcq_default_planner_params.  The session keeps ctx (and its stream). */
+int mpcq_session_create(mpcq_ctx* ctx, int64_t batch, const mpcq_planner_params* pp,
+                        const double* gait0, mpcq_session** out);
+int mpcq_session_destroy(mpcq_session* s);
+
+/* One tick for every robot.  state [B][12] (lC, abg, lV, lW), l_feet [B][3][4],
+ * v_ref [B][6], reduced [B] (NULL = 0); host pointers, or device pointers with
+ * MPCQ_FLAG_DEVICE_PTRS.  state / l_feet NULL = the virtual robot (above).
+ * k = MPC tick index (k == 0: first tick, MPC.py:491).  Blocking unless
+ * MPCQ_FLAG_ASYNC together with MPCQ_FLAG_DEVICE_PTRS. */
+int mpcq_session_tick(mpcq_session* s, int k, const double* state, const double* l_feet,
+                      const double* v_ref, const int32_t* reduced, uint32_t flags);
+
+/* Per-robot arrays a session holds (mpcq_session_read / mpcq_session_device_ptr). */
+#define MPCQ_SV_F0 0        /* [B][12]     f_applied (MPC.py:441-444) */
+#define MPCQ_SV_X 1         /* [B][24N]    QP solution x */
+#define MPCQ_SV_X_ROBOT 2   /* [B][12][N]  x_robot = x states + xref[:, 1:] (MPC.py:437-449) */
+#define MPCQ_SV_Q_W 3       /* [B][6]      world pose (MPC.py:503-510) */
+#define MPCQ_SV_COST 4      /* [B][13]     Logger.log_cost_function (Logger.py:406-418) */
+#define MPCQ_SV_XREF 5      /* [B][12][N+1] */
+#define MPCQ_SV_FSTEPS 6    /* [B][20][13] */
+#define MPCQ_SV_GAIT 7      /* [B][20][5] */
+#define MPCQ_SV_STATUS 8    /* [B] int32: OSQP status, or MPCQ_STATUS_BAD_GAIT from the planner */
+#define MPCQ_SV_ITERS 9     /* [B] int32 */
+#define MPCQ_SV_RHO 10      /* [B] */
+#define MPCQ_SV_Y 11        /* [B][44N] */
+#define MPCQ_SV_STATE 12    /* [B][12]     the virtual robot's next state */
+#define MPCQ_SV_L_FEET 13   /* [B][3][4]   the virtual robot's next feet */
+#define MPCQ_SV_ROT_FLAG 14 /* [B] int32 */
+#define MPCQ_SV_H_ROT 15    /* [B] */
+#define MPCQ_SV_COUNT 16
+/* Copy array `what` to dst (host, or device with MPCQ_FLAG_DEVICE_PTRS); blocking. */
+int mpcq_session_read(mpcq_session* s, int what, void* dst, uint32_t flags);
+/* Overwrite array `what` from src (host, or device with MPCQ_FLAG_DEVICE_PTRS); blocking. */
+int mpcq_session_write(mpcq_session* s, int what, const void* src, uint32_t flags);
+/* Device address of array `what` (valid until mpcq_session_destroy). */
+int mpcq_session_device_ptr(mpcq_session* s, int what, void** out);
+
 /* ---- diagnostics -----------------------------------------------------------
  * Device buffer [B][16] (uint64) that a diagnostic build of the library
  * (compiled with -DMPCQ_STAMPS, libmpcq_stamps.so) fills with per-phase

@@ -5,6 +5,7 @@
 // (mpcq_kernels.hip); there is no CPU fallback: a missing device is an error.
 #include <math.h>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -473,6 +474,305 @@ int mpcq_plan_batch(mpcq_ctx* c, const mpcq_planner_params* pp, int64_t B, uint3
   HIP_TRY(mpcq::launch_plan(P, a, c->stream));
   if (!dev) return unstage(c, xs, NX);
   if (!(flags & MPCQ_FLAG_ASYNC)) HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPCQ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Closed-loop session: per-robot state resident in HBM (include/mpcq.h).
+
+}  // extern "C"
+
+struct mpcq_session {
+  mpcq_ctx* ctx = nullptr;
+  int64_t B = 0;
+  mpcq_planner_params pp{};
+  void* mem = nullptr;
+  void* arr[MPCQ_SV_COUNT] = {};
+  size_t bytes[MPCQ_SV_COUNT] = {};
+  double* warm_x = nullptr;
+  int32_t* plan_status = nullptr;
+  int32_t* info = nullptr;
+  double* in_state = nullptr;   // staging of host inputs
+  double* in_lfeet = nullptr;
+  double* in_vref = nullptr;
+  int32_t* in_reduced = nullptr;
+};
+
+namespace {
+
+size_t sv_bytes(int what, int64_t B, int N) {
+  const size_t b = (size_t)B;
+  switch (what) {
+    case MPCQ_SV_F0: return b * 12 * 8;
+    case MPCQ_SV_X: return b * 24 * N * 8;
+    case MPCQ_SV_X_ROBOT: return b * 12 * N * 8;
+    case MPCQ_SV_Q_W: return b * 6 * 8;
+    case MPCQ_SV_COST: return b * 13 * 8;
+    case MPCQ_SV_XREF: return b * 12 * (N + 1) * 8;
+    case MPCQ_SV_FSTEPS: return b * 260 * 8;
+    case MPCQ_SV_GAIT: return b * 100 * 8;
+    case MPCQ_SV_STATUS: return b * 4;
+    case MPCQ_SV_ITERS: return b * 4;
+    case MPCQ_SV_RHO: return b * 8;
+    case MPCQ_SV_Y: return b * 44 * N * 8;
+    case MPCQ_SV_STATE: return b * 12 * 8;
+    case MPCQ_SV_L_FEET: return b * 12 * 8;
+    case MPCQ_SV_ROT_FLAG: return b * 4;
+    case MPCQ_SV_H_ROT: return b * 8;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpcq_session_create(mpcq_ctx* c, int64_t B, const mpcq_planner_params* pp, const double* gait0,
+                        mpcq_session** out) {
+  if (!out) return fail(MPCQ_E_INVALID, "out is NULL");
+  *out = nullptr;
+  int rc = check_ctx(c, B);
+  if (rc) return rc;
+  if (B < 1) return fail(MPCQ_E_INVALID, "a session needs batch >= 1");
+  const int N = c->N;
+  mpcq_session* s = new mpcq_session();
+  s->ctx = c;
+  s->B = B;
+  if (pp) s->pp = *pp;
+  else mpcq_default_planner_params(&s->pp);
+  // one allocation: the named arrays, then the private ones
+  size_t off[MPCQ_SV_COUNT + 8];
+  size_t tot = 0;
+  auto take = [&](size_t nb) { size_t o = tot; tot += (nb + 255) & ~size_t(255); return o; };
+  for (int w = 0; w < MPCQ_SV_COUNT; ++w) { s->bytes[w] = sv_bytes(w, B, N); off[w] = take(s->bytes[w]); }
+  const size_t o_wx = take((size_t)B * 24 * N * 8), o_ps = take((size_t)B * 4), o_in = take((size_t)B * 16),
+               o_st = take((size_t)B * 96), o_lf = take((size_t)B * 96), o_vr = take((size_t)B * 48),
+               o_rd = take((size_t)B * 4);
+  DeviceGuard g(c->device);
+  if (hipMalloc(&s->mem, tot) != hipSuccess) {
+    delete s;
+    return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) for the session failed", tot);
+  }
+  char* base = (char*)s->mem;
+  for (int w = 0; w < MPCQ_SV_COUNT; ++w) s->arr[w] = base + off[w];
+  s->warm_x = (double*)(base + o_wx);
+  s->plan_status = (int32_t*)(base + o_ps);
+  s->info = (int32_t*)(base + o_in);
+  s->in_state = (double*)(base + o_st);
+  s->in_lfeet = (double*)(base + o_lf);
+  s->in_vref = (double*)(base + o_vr);
+  s->in_reduced = (int32_t*)(base + o_rd);
+  // initial values: the reference objects' constructors
+  const size_t hb = sv_bytes(MPCQ_SV_XREF, B, N) > sv_bytes(MPCQ_SV_FSTEPS, B, N) ? sv_bytes(MPCQ_SV_XREF, B, N)
+                                                                                  : sv_bytes(MPCQ_SV_FSTEPS, B, N);
+  double* h = (double*)malloc(hb > (size_t)B * 100 * 8 ? hb : (size_t)B * 100 * 8);
+  int32_t* hi = (int32_t*)malloc((size_t)B * 4);
+  if (!h || !hi) { free(h); free(hi); mpcq_session_destroy(s); return fail(MPCQ_E_NOMEM, "host malloc failed"); }
+  int err = 0;
+  auto put = [&](int w, const void* src) {
+    if (!err && hipMemcpy(s->arr[w], src, s->bytes[w], hipMemcpyHostToDevice) != hipSuccess) err = 1;
+  };
+  if (gait0) {
+    put(MPCQ_SV_GAIT, gait0);
+  } else {  // create_walking_trot (FootstepPlanner.py:193-214): [1, 7, 1, 7] per 16-step period
+    const int half = (int)(0.5 * s->pp.T_gait / s->pp.dt);
+    const int per = 2 * half, nper = per > 0 ? N / per : 0;
+    if (nper < 1 || nper * per != N || 4 * nper > 19) {
+      free(h); free(hi); mpcq_session_destroy(s);
+      return fail(MPCQ_E_INVALID, "no walking-trot table for N=%d with T_gait/dt = %d; pass gait0", N, per);
+    }
+    for (int64_t b = 0; b < B; ++b) {
+      double* gt = h + b * 100;
+      for (int e = 0; e < 100; ++e) gt[e] = 0.0;
+      for (int i = 0; i < nper; ++i) {
+        const double d[4] = {1.0, half - 1.0, 1.0, half - 1.0};
+        const int m[4][4] = {{1, 1, 1, 1}, {1, 0, 0, 1}, {1, 1, 1, 1}, {0, 1, 1, 0}};
+        for (int r = 0; r < 4; ++r) {
+          gt[5 * (4 * i + r)] = d[r];
+          for (int q = 0; q < 4; ++q) gt[5 * (4 * i + r) + 1 + q] = m[r][q];
+        }
+      }
+    }
+    put(MPCQ_SV_GAIT, h);
+  }
+  for (size_t e = 0; e < (size_t)B * 12 * (N + 1); ++e) h[e] = 0.0;
+  put(MPCQ_SV_XREF, h);  // FootstepPlanner.py:58
+  for (int64_t b = 0; b < B; ++b) {
+    double* q = h + b * 6;  // MPC.py:53-56
+    q[0] = 0.0; q[1] = 0.0; q[2] = 0.2027682; q[3] = 0.0; q[4] = 0.0; q[5] = 0.0;
+  }
+  put(MPCQ_SV_Q_W, h);
+  for (int64_t b = 0; b < B; ++b) {  // virtual robot standing at h_ref, feet under the shoulders
+    double* st = h + b * 12;
+    for (int e = 0; e < 12; ++e) st[e] = 0.0;
+    st[2] = s->pp.h_ref;
+  }
+  put(MPCQ_SV_STATE, h);
+  for (int64_t b = 0; b < B; ++b) {
+    double* lf = h + b * 12;
+    for (int q = 0; q < 4; ++q) { lf[q] = s->pp.shoulders[q]; lf[4 + q] = s->pp.shoulders[4 + q]; lf[8 + q] = 0.0; }
+  }
+  put(MPCQ_SV_L_FEET, h);
+  for (int64_t b = 0; b < B; ++b) h[b] = 0.20;  // FootstepPlanner.py:68
+  put(MPCQ_SV_H_ROT, h);
+  for (int64_t b = 0; b < B; ++b) h[b] = c->p.rho;
+  put(MPCQ_SV_RHO, h);
+  for (int64_t b = 0; b < B; ++b) hi[b] = 0;
+  put(MPCQ_SV_ROT_FLAG, hi);
+  put(MPCQ_SV_STATUS, hi);
+  put(MPCQ_SV_ITERS, hi);
+  for (size_t e = 0; e < (size_t)B * 260; ++e) h[e] = NAN;
+  put(MPCQ_SV_FSTEPS, h);
+  free(h);
+  free(hi);
+  if (!err && hipMemset(s->arr[MPCQ_SV_X], 0, s->bytes[MPCQ_SV_X]) != hipSuccess) err = 1;
+  if (!err && hipMemset(s->arr[MPCQ_SV_Y], 0, s->bytes[MPCQ_SV_Y]) != hipSuccess) err = 1;
+  if (!err && hipMemset(s->warm_x, 0, (size_t)B * 24 * N * 8) != hipSuccess) err = 1;
+  if (err) { mpcq_session_destroy(s); return fail(MPCQ_E_DEVICE, "initialising the session failed"); }
+  *out = s;
+  return MPCQ_OK;
+}
+
+int mpcq_session_destroy(mpcq_session* s) {
+  if (!s) return MPCQ_OK;
+  if (s->mem) {
+    DeviceGuard g(s->ctx->device);
+    (void)hipStreamSynchronize(s->ctx->stream);
+    (void)hipFree(s->mem);
+  }
+  delete s;
+  return MPCQ_OK;
+}
+
+int mpcq_session_tick(mpcq_session* s, int k, const double* state, const double* l_feet, const double* v_ref,
+                      const int32_t* reduced, uint32_t flags) {
+  if (!s) return fail(MPCQ_E_INVALID, "session is NULL");
+  if (!v_ref) return fail(MPCQ_E_INVALID, "v_ref is required");
+  if (k < 0) return fail(MPCQ_E_INVALID, "k must be >= 0");
+  mpcq_ctx* c = s->ctx;
+  DeviceGuard g(c->device);
+  const int N = c->N;
+  const int64_t B = s->B;
+  const bool dev = flags & MPCQ_FLAG_DEVICE_PTRS;
+  auto in = [&](const void* src, void* stage_buf, size_t nb) -> const void* {
+    if (!src) return nullptr;
+    if (dev) return src;
+    if (hipMemcpyAsync(stage_buf, src, nb, hipMemcpyHostToDevice, c->stream) != hipSuccess) return nullptr;
+    return stage_buf;
+  };
+  const double* st = state ? (const double*)in(state, s->in_state, (size_t)B * 96) : (const double*)s->arr[MPCQ_SV_STATE];
+  const double* lf = l_feet ? (const double*)in(l_feet, s->in_lfeet, (size_t)B * 96) : (const double*)s->arr[MPCQ_SV_L_FEET];
+  const double* vr = (const double*)in(v_ref, s->in_vref, (size_t)B * 48);
+  const int32_t* rd = reduced ? (const int32_t*)in(reduced, s->in_reduced, (size_t)B * 4) : nullptr;
+  if (!st || !lf || !vr || (reduced && !rd)) return fail(MPCQ_E_DEVICE, "staging the tick inputs failed");
+  // the virtual robot's state lives in buffers the retrieve kernel rewrites:
+  // this tick reads a copy
+  if (!state) {
+    HIP_TRY(hipMemcpyAsync(s->in_state, st, (size_t)B * 96, hipMemcpyDeviceToDevice, c->stream));
+    st = s->in_state;
+  }
+  if (!l_feet) {
+    HIP_TRY(hipMemcpyAsync(s->in_lfeet, lf, (size_t)B * 96, hipMemcpyDeviceToDevice, c->stream));
+    lf = s->in_lfeet;
+  }
+  // 1. planner (processing.py:80-89, 131)
+  mpcq::PlanArgs pa{};
+  pa.batch = B;
+  pa.N = N;
+  pa.k = k;
+  pa.state = st;
+  pa.l_feet = lf;
+  pa.v_ref = vr;
+  pa.reduced = rd;
+  pa.gait = (double*)s->arr[MPCQ_SV_GAIT];
+  pa.rot_flag = (int32_t*)s->arr[MPCQ_SV_ROT_FLAG];
+  pa.h_rot = (double*)s->arr[MPCQ_SV_H_ROT];
+  pa.xref = (double*)s->arr[MPCQ_SV_XREF];
+  pa.fsteps = (double*)s->arr[MPCQ_SV_FSTEPS];
+  pa.status = s->plan_status;
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  if (k == 0) {  // update_fsteps(0, ...): no roll
+    pa.ops = MPCQ_PLAN_FOOTSTEPS;
+    HIP_TRY(mpcq::launch_plan(s->pp, pa, c->stream));
+  }
+  pa.ops = MPCQ_PLAN_TICK;
+  HIP_TRY(mpcq::launch_plan(s->pp, pa, c->stream));
+  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+  c->have_form = true;
+  // 2. MPC.run: formulation + OSQP solve (warm from the previous tick when k > 0)
+  mpcq::LaunchArgs la{};
+  la.batch = B;
+  la.mode = k == 0 ? MPCQ_MODE_SETUP : MPCQ_MODE_UPDATE;
+  la.xref = (const double*)s->arr[MPCQ_SV_XREF];
+  la.fsteps = (const double*)s->arr[MPCQ_SV_FSTEPS];
+  if (k > 0) {
+    la.warm_x = s->warm_x;
+    la.warm_y = (const double*)s->arr[MPCQ_SV_Y];
+    la.rho_in = (const double*)s->arr[MPCQ_SV_RHO];
+  }
+  la.f0 = (double*)s->arr[MPCQ_SV_F0];
+  la.x = (double*)s->arr[MPCQ_SV_X];
+  la.y = (double*)s->arr[MPCQ_SV_Y];
+  la.status = (int32_t*)s->arr[MPCQ_SV_STATUS];
+  la.iters = (int32_t*)s->arr[MPCQ_SV_ITERS];
+  la.rho_out = (double*)s->arr[MPCQ_SV_RHO];
+  la.info = s->info;
+  la.stamps = c->stamps;
+  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  HIP_TRY(mpcq::launch_solve(N, true, c->p, la, c->stream));
+  HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+  c->have_solve = true;
+  // 3. retrieve_result, q_w, Logger cost, next warm start, virtual robot
+  mpcq::SessionArgs ra{};
+  ra.batch = B;
+  ra.x = (const double*)s->arr[MPCQ_SV_X];
+  ra.xref = (const double*)s->arr[MPCQ_SV_XREF];
+  ra.fsteps = (const double*)s->arr[MPCQ_SV_FSTEPS];
+  ra.gait = (const double*)s->arr[MPCQ_SV_GAIT];
+  ra.status = (int32_t*)s->arr[MPCQ_SV_STATUS];
+  ra.plan_status = s->plan_status;
+  ra.x_robot = (double*)s->arr[MPCQ_SV_X_ROBOT];
+  ra.warm_x = s->warm_x;
+  ra.y = (double*)s->arr[MPCQ_SV_Y];
+  ra.rho = (double*)s->arr[MPCQ_SV_RHO];
+  ra.rho0 = c->p.rho;
+  ra.cost = (double*)s->arr[MPCQ_SV_COST];
+  ra.q_w = (double*)s->arr[MPCQ_SV_Q_W];
+  ra.next_state = (double*)s->arr[MPCQ_SV_STATE];
+  ra.next_l_feet = (double*)s->arr[MPCQ_SV_L_FEET];
+  for (int i = 0; i < 12; ++i) ra.state_weights[i] = c->p.state_weights[i];
+  ra.force_weight = c->p.force_weight;
+  for (int i = 0; i < 8; ++i) ra.shoulders[i] = s->pp.shoulders[i];
+  HIP_TRY(mpcq::launch_retrieve(N, ra, c->stream));
+  // host inputs are staged in buffers the next tick reuses: host calls block
+  if (!(flags & MPCQ_FLAG_ASYNC) || !dev) HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPCQ_OK;
+}
+
+int mpcq_session_read(mpcq_session* s, int what, void* dst, uint32_t flags) {
+  if (!s || !dst) return fail(MPCQ_E_INVALID, "NULL argument");
+  if (what < 0 || what >= MPCQ_SV_COUNT) return fail(MPCQ_E_INVALID, "unknown session array %d", what);
+  DeviceGuard g(s->ctx->device);
+  const hipMemcpyKind kind = (flags & MPCQ_FLAG_DEVICE_PTRS) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  HIP_TRY(hipMemcpyAsync(dst, s->arr[what], s->bytes[what], kind, s->ctx->stream));
+  HIP_TRY(hipStreamSynchronize(s->ctx->stream));
+  return MPCQ_OK;
+}
+
+int mpcq_session_write(mpcq_session* s, int what, const void* src, uint32_t flags) {
+  if (!s || !src) return fail(MPCQ_E_INVALID, "NULL argument");
+  if (what < 0 || what >= MPCQ_SV_COUNT) return fail(MPCQ_E_INVALID, "unknown session array %d", what);
+  DeviceGuard g(s->ctx->device);
+  const hipMemcpyKind kind = (flags & MPCQ_FLAG_DEVICE_PTRS) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  HIP_TRY(hipMemcpyAsync(s->arr[what], src, s->bytes[what], kind, s->ctx->stream));
+  HIP_TRY(hipStreamSynchronize(s->ctx->stream));
+  return MPCQ_OK;
+}
+
+int mpcq_session_device_ptr(mpcq_session* s, int what, void** out) {
+  if (!s || !out) return fail(MPCQ_E_INVALID, "NULL argument");
+  if (what < 0 || what >= MPCQ_SV_COUNT) return fail(MPCQ_E_INVALID, "unknown session array %d", what);
+  *out = s->arr[what];
   return MPCQ_OK;
 }
 

@@ -55,6 +55,31 @@ struct PlanArgs {
 
 hipError_t launch_plan(const mpcq_planner_params& pp, const PlanArgs& a, hipStream_t s);
 
+// Session epilogue (mpcq_session.hip): one robot per wave64.
+struct SessionArgs {
+  int64_t batch;
+  const double* x;       // [B][24N] solution of this tick
+  const double* xref;    // [B][12][N+1]
+  const double* fsteps;  // [B][20][13]
+  const double* gait;    // [B][20][5]
+  int32_t* status;       // [B] engine status, overridden by a planner failure
+  const int32_t* plan_status;  // [B]
+  double* x_robot;       // [B][12][N]
+  double* warm_x;        // [B][24N] next tick's warm start
+  double* y;             // [B][44N] reset to 0 after a failed solve
+  double* rho;           // [B]      reset to rho0 after a failed solve
+  double rho0;
+  double* cost;          // [B][13]
+  double* q_w;           // [B][6]
+  double* next_state;    // [B][12]
+  double* next_l_feet;   // [B][3][4]
+  double state_weights[12];
+  double force_weight;
+  double shoulders[8];
+};
+
+hipError_t launch_retrieve(int N, const SessionArgs& a, hipStream_t s);
+
 // Launchers (mpcq_engine.hip).  Return hipError_t.
 hipError_t launch_formulate(int N, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);
 hipError_t launch_solve(int N, bool fused, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);

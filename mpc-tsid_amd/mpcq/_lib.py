@@ -3,6 +3,12 @@
 The shared library is built in-tree (mpc-tsid_amd/csrc/Makefile ->
 mpc-tsid_amd/mpcq/libmpcq.so) and loaded from here.  There is no fallback:
 if the library or a HIP device is missing, the calls raise.
+
+A process that also uses torch.cuda (device-pointer entry points on torch
+tensors) must ``import torch`` before the first call here: torch bundles its
+own HIP runtime, and libmpcq.so then binds to it (same sonames).  Loaded the
+other way round, two runtimes end up in the process and torch sees no device
+(tools/diag_runtime.py).
 """
 from __future__ import annotations
 
@@ -32,12 +38,16 @@ MODE_UPDATE = 0
 MODE_SETUP = 1
 PLAN_ROLL, PLAN_FOOTSTEPS, PLAN_REFSTATES = 1, 2, 4
 PLAN_TICK = PLAN_ROLL | PLAN_FOOTSTEPS | PLAN_REFSTATES
+# closed-loop session arrays (MPCQ_SV_*)
+SV_F0, SV_X, SV_X_ROBOT, SV_Q_W, SV_COST, SV_XREF, SV_FSTEPS, SV_GAIT = range(8)
+SV_STATUS, SV_ITERS, SV_RHO, SV_Y, SV_STATE, SV_L_FEET, SV_ROT_FLAG, SV_H_ROT = range(8, 16)
 
 EXPORTS = ("mpcq_abi_version", "mpcq_default_params", "mpcq_dims", "mpcq_pattern",
            "mpcq_supported_horizons", "mpcq_last_error", "mpcq_create", "mpcq_destroy",
            "mpcq_set_stream", "mpcq_last_kernel_ms", "mpcq_formulate_batch",
            "mpcq_qp_solve_batch", "mpcq_solve_batch", "mpcq_default_planner_params",
-           "mpcq_plan_batch", "mpcq_debug_set_stamps")
+           "mpcq_plan_batch", "mpcq_session_create", "mpcq_session_destroy", "mpcq_session_tick",
+           "mpcq_session_read", "mpcq_session_write", "mpcq_session_device_ptr", "mpcq_debug_set_stamps")
 
 
 class MpcqError(RuntimeError):
@@ -141,11 +151,18 @@ def lib():
     L.mpcq_debug_set_stamps.argtypes = [vp, vp]
     L.mpcq_default_planner_params.argtypes = [C.POINTER(PlannerParams)]
     L.mpcq_default_planner_params.restype = None
+    L.mpcq_session_create.argtypes = [vp, C.c_int64, C.POINTER(PlannerParams), vp, C.POINTER(vp)]
+    L.mpcq_session_destroy.argtypes = [vp]
+    L.mpcq_session_tick.argtypes = [vp, C.c_int, vp, vp, vp, vp, C.c_uint32]
+    L.mpcq_session_read.argtypes = [vp, C.c_int, vp, C.c_uint32]
+    L.mpcq_session_write.argtypes = [vp, C.c_int, vp, C.c_uint32]
+    L.mpcq_session_device_ptr.argtypes = [vp, C.c_int, C.POINTER(vp)]
     L.mpcq_plan_batch.argtypes = [vp, C.POINTER(PlannerParams), C.c_int64, C.c_uint32, C.c_int] + [vp] * 12 + [C.c_uint32]
     for name in ("mpcq_dims", "mpcq_pattern", "mpcq_supported_horizons", "mpcq_create",
                  "mpcq_destroy", "mpcq_set_stream", "mpcq_last_kernel_ms", "mpcq_formulate_batch",
                  "mpcq_qp_solve_batch", "mpcq_solve_batch", "mpcq_default_planner_params",
-           "mpcq_plan_batch", "mpcq_debug_set_stamps"):
+           "mpcq_plan_batch", "mpcq_session_create", "mpcq_session_destroy", "mpcq_session_tick",
+           "mpcq_session_read", "mpcq_session_write", "mpcq_session_device_ptr", "mpcq_debug_set_stamps"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

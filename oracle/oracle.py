@@ -98,6 +98,8 @@ def lib():
                                          dp, dp, ip, ip, C.c_int]
         L.oracle_num_threads.restype = C.c_int
         L.oracle_default_planner_params.argtypes = [C.POINTER(PlannerParams)]
+        L.oracle_retrieve.argtypes = [C.POINTER(Params), C.c_int, dp, dp, dp, dp, dp, C.c_int,
+                                      dp, dp, dp, dp, dp, dp]
         L.oracle_plan.argtypes = [C.POINTER(PlannerParams), C.c_int, C.c_uint, C.c_int, dp, dp, dp, dp, dp,
                                   C.c_int, dp, ip, dp, dp, dp]
         _lib = L
@@ -223,6 +225,80 @@ class Planner:
 
 PLAN_ROLL, PLAN_FOOTSTEPS, PLAN_REFSTATES = 1, 2, 4
 PLAN_TICK = 7
+
+
+def retrieve(N, x, xref, fsteps, gait, q_w, failed=False, params: Params | None = None,
+             shoulders=None):
+    """session_oracle.c: x_robot, q_w (updated copy), cost, next warm start, virtual robot."""
+    p = params or default_params()
+    sh = np.ascontiguousarray(shoulders if shoulders is not None else
+                              [0.19, 0.19, -0.19, -0.19, 0.15005, -0.15005, 0.15005, -0.15005], np.float64)
+    x = np.ascontiguousarray(x, np.float64)
+    xref = np.ascontiguousarray(xref, np.float64)
+    fsteps = np.ascontiguousarray(fsteps, np.float64)
+    gait = np.ascontiguousarray(gait, np.float64)
+    qw = np.array(q_w, np.float64).ravel().copy()
+    out = dict(x_robot=np.zeros((12, N)), cost=np.zeros(13), warm_x=np.zeros(24 * N), state=np.zeros(12),
+               l_feet=np.zeros((3, 4)))
+    lib().oracle_retrieve(C.byref(p), N, _dp(x), _dp(xref), _dp(fsteps), _dp(gait), _dp(sh), int(bool(failed)),
+                          _dp(out["x_robot"]), _dp(qw), _dp(out["cost"]), _dp(out["warm_x"]), _dp(out["state"]),
+                          _dp(out["l_feet"]))
+    out["q_w"] = qw
+    return out
+
+
+class Session:
+    """One robot's closed loop as the reference runs it (processing.py:80-131 +
+    MPC.run, MPC.py:460-514), composed from the restatements: planner ->
+    formulation -> OSQP (warm from the previous tick: shifted x, y and rho as
+    osqp keeps them) -> retrieve / q_w / cost -> virtual robot."""
+
+    def __init__(self, N, gait0, params: Params | None = None, planner_params: PlannerParams | None = None):
+        self.N = N
+        self.p = params or default_params()
+        self.planner = Planner(N, gait0, planner_params)
+        self.x = np.zeros(24 * N)
+        self.y = np.zeros(44 * N)
+        self.rho = self.p.rho
+        self.warm_x = np.zeros(24 * N)
+        self.q_w = np.array([0.0, 0.0, 0.2027682, 0.0, 0.0, 0.0])
+        self.state = np.zeros(12)
+        self.state[2] = self.planner.p.h_ref
+        sh = np.array(self.planner.p.shoulders[:]).reshape(2, 4)
+        self.l_feet = np.vstack([sh, np.zeros((1, 4))])
+        self.status = 0
+        self.iters = 0
+
+    def tick(self, k, v_ref, state=None, l_feet=None, reduced=False):
+        st = self.state if state is None else np.asarray(state, np.float64).ravel()
+        lf = self.l_feet if l_feet is None else np.asarray(l_feet, np.float64).reshape(3, 4)
+        pst = 0
+        if k == 0:
+            pst = self.planner.plan(PLAN_FOOTSTEPS, 0, st, lf, v_ref, reduced)
+        pst = self.planner.plan(PLAN_TICK, k, st, lf, v_ref, reduced) or pst
+        N = self.N
+        mode = 1 if k == 0 else 0
+        Ax, l, u = formulate(self.planner.xref, self.planner.fsteps, mode, self.p)
+        if k == 0:
+            r = qp_solve(N, Ax, l, u, self.p)
+        else:
+            r = qp_solve(N, Ax, l, u, self.p, warm_x=self.warm_x, warm_y=self.y, rho=self.rho)
+        self.x, self.y, self.rho = r["x"], r["y"], r["rho"]
+        self.status, self.iters = r["status"], r["iters"]
+        failed = self.status not in (1, 2, -2)
+        o = retrieve(N, self.x, self.planner.xref, self.planner.fsteps, self.planner.gait, self.q_w, failed,
+                     self.p, self.planner.p.shoulders[:])
+        self.x_robot, self.cost, self.warm_x = o["x_robot"], o["cost"], o["warm_x"]
+        if failed:
+            self.y = np.zeros(44 * N)
+            self.rho = self.p.rho
+        else:
+            self.q_w = o["q_w"]
+            self.state, self.l_feet = o["state"], o["l_feet"]
+        if pst:
+            self.status = pst
+        self.f0 = self.x[12 * N:12 * N + 12]
+        return self.status
 
 
 def num_threads() -> int:

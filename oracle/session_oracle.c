@@ -1,0 +1,110 @@
+/*
+ * session_oracle.c — CPU restatement of what the reference does with a QP
+ * solution between two solves.  TEST INFRASTRUCTURE ONLY: the checker of the
+ * session epilogue (mpc-tsid_amd/csrc/mpcq_session.hip); never linked by the
+ * product.
+ *
+ *   retrieve_result          MPC.py:432-458 (x_robot = x states + xref[:, 1:])
+ *   world pose q_w           MPC.py:503-510 (np.dot(R, q_next[0:2]) as BLAS
+ *                            evaluates it: fma(R[i,0], q0, R[i,1] * q1))
+ *   next warm start          MPC.py:403-406 (states shifted one stage, last
+ *                            zeroed; forces rolled with wrap-around)
+ *   log_cost_function        Logger.py:406-418 ((x_i P_i) x_i, summed with
+ *                            numpy's pairwise summation)
+ *   virtual robot            the next tick's local-frame state and feet from
+ *                            x_robot[:, 0] (a harness, not a reference
+ *                            function: processing.py:33-38 is its precedent)
+ * Pinned by tests/golden/session_golden.npz (gen_session_golden.py), captured
+ * from the unmodified MPC.py / Logger.py on prescribed solutions x.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../include/mpcq.h"
+
+/* numpy pairwise_sum over v[0], v[s], ..., v[(n-1)s] */
+static double pairwise(const double* v, int n, int s) {
+  if (n < 8) {
+    double r = -0.0;
+    for (int i = 0; i < n; ++i) r += v[i * s];
+    return r;
+  }
+  if (n <= 128) {
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = v[j * s];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += v[(i + j) * s];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += v[i * s];
+    return res;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return pairwise(v, n2, s) + pairwise(v + n2 * s, n - n2, s);
+}
+
+/* One robot.  x [24N], xref [12][N+1], fsteps / gait after this tick's planner.
+ * Outputs: x_robot [12][N], q_w [6] (in/out), cost [13], warm_x [24N],
+ * next_state [12], next_l_feet [3][4].  failed: a solve whose x is unusable. */
+void oracle_retrieve(const mpcq_params* p, int N, const double* x, const double* xref,
+                     const double* fsteps, const double* gait, const double* shoulders, int failed,
+                     double* x_robot, double* q_w, double* cost, double* warm_x, double* next_state,
+                     double* next_l_feet) {
+  const int NP = N + 1, n = 24 * N;
+  for (int r = 0; r < 12; ++r)
+    for (int k = 0; k < N; ++k) x_robot[r * N + k] = x[12 * k + r] + xref[r * NP + k + 1];
+  for (int e = 0; e < n; ++e) {
+    double v;
+    if (e < 12 * N) v = e < 12 * (N - 1) ? x[e + 12] : 0.0;
+    else v = x[12 * N + (e - 12 * N + 12) % (12 * N)];
+    warm_x[e] = failed ? 0.0 : v;
+  }
+  double c[24 * 32];
+  for (int e = 0; e < n; ++e) {
+    const double w = e < 12 * N ? p->state_weights[e % 12] : p->force_weight;
+    c[e] = (x[e] * w) * x[e];
+  }
+  for (int r = 0; r < 12; ++r) cost[r] = pairwise(c + r, N, 12);
+  cost[12] = pairwise(c + 12 * N, 12 * N, 1);
+  if (failed) return;
+  double qn[12];
+  for (int r = 0; r < 12; ++r) qn[r] = x_robot[r * N];
+  const double co = cos(q_w[5]), si = sin(q_w[5]);
+  const double d0 = fma(co, qn[0], (-si) * qn[1]);
+  const double d1 = fma(si, qn[0], co * qn[1]);
+  q_w[0] = q_w[0] + d0;
+  q_w[1] = q_w[1] + d1;
+  q_w[2] = qn[2];
+  q_w[3] = qn[3];
+  q_w[4] = qn[4];
+  q_w[5] = q_w[5] + qn[5];
+  /* virtual robot: the local frame moves under the predicted base, yaw removed
+     (Interface.py:100-138); velocities rotated into it */
+  const double cy = cos(qn[5]), sy = sin(qn[5]);
+  double* ns = next_state;
+  ns[0] = 0.0; ns[1] = 0.0; ns[2] = qn[2];
+  ns[3] = qn[3]; ns[4] = qn[4]; ns[5] = 0.0;
+  ns[6] = cy * qn[6] + sy * qn[7];
+  ns[7] = -sy * qn[6] + cy * qn[7];
+  ns[8] = qn[8];
+  ns[9] = cy * qn[9] + sy * qn[10];
+  ns[10] = -sy * qn[9] + cy * qn[10];
+  ns[11] = qn[11];
+  /* feet in stance after the next roll: fsteps row 0 if the current phase goes
+     on, row 1 if it ends (FootstepPlanner.py:418-423); swing feet under the shoulders */
+  const int row = gait[0] > 1.0 ? 0 : 1;
+  for (int q = 0; q < 4; ++q) {
+    double px = fsteps[13 * row + 1 + 3 * q], py = fsteps[13 * row + 2 + 3 * q], pz = fsteps[13 * row + 3 + 3 * q];
+    if (isnan(px) || isnan(py) || isnan(pz)) {
+      px = shoulders[q] + qn[0];
+      py = shoulders[4 + q] + qn[1];
+      pz = 0.0;
+    }
+    const double dx = px - qn[0], dy = py - qn[1];
+    next_l_feet[q] = cy * dx + sy * dy;
+    next_l_feet[4 + q] = -sy * dx + cy * dy;
+    next_l_feet[8 + q] = pz;
+  }
+}

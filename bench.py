@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--gather", action="store_true", help="include an RCCL all-gather of f0 in the timed region")
     ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--mode", default="qp", choices=("qp", "plan", "tick"),
+                    help="qp: the headline (fused formulation + OSQP per instance); plan: the batched "
+                         "FootstepPlanner kernel alone; tick: closed-loop sessions (planner + warm-started "
+                         "solve + retrieve per robot and tick, virtual robot)")
     return ap.parse_args()
 
 
@@ -73,8 +77,186 @@ def load_traffic(tag: str):
         return None
 
 
+def _dist_setup():
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    return torch, dist, world, rank, local, dev
+
+
+def _timed(torch, dist, dev, world, stream, step, steps, warmup):
+    """W untimed steps, then K steps between barriers + synchronisations; returns
+    (max-over-ranks wall seconds, HIP-event ms per step on the launch stream)."""
+    from mpcq import shard
+    torch.cuda.set_stream(stream)
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(steps):
+        step(warmup + i)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    return shard.max_over_ranks(dist, wall, dev, world), ev0.elapsed_time(ev1) / max(steps, 1)
+
+
+def main_plan(args):
+    """Batched FootstepPlanner (mpcq_plan_batch, MPCQ_PLAN_TICK) on device-resident
+    robots: one step = one planner launch over this rank's robots."""
+    torch, dist, world, rank, local, dev = _dist_setup()
+    import mpcq
+    from mpcq import model, synth
+    N = CONFIGS[args.config]["N"]
+    per = args.batch or 65536
+    rng = np.random.default_rng(args.seed + rank)
+    gaits = np.stack([synth.gait_table(("trot", "bound", "pace")[b % 3], N) for b in range(per)])
+    state = np.concatenate([np.zeros((per, 2)), 0.2 + rng.uniform(-.01, .01, (per, 1)), rng.normal(0, .02, (per, 2)),
+                            np.zeros((per, 1)), rng.normal(0, .2, (per, 6))], axis=1)
+    sh = np.array([[0.19, 0.19, -0.19, -0.19], [0.15005, -0.15005, 0.15005, -0.15005]])
+    l_feet = np.concatenate([sh + rng.uniform(-.03, .03, (per, 2, 4)), np.zeros((per, 1, 4))], axis=1)
+    v_ref = np.stack([rng.uniform(-.5, 1, per), rng.uniform(-.3, .3, per), np.zeros(per), rng.normal(0, .1, per),
+                      rng.normal(0, .1, per), rng.uniform(-.5, .5, per)], axis=1)
+    T = lambda a, dt=torch.float64: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
+    d = dict(state=T(state), l_feet=T(l_feet), v_ref=T(v_ref), gait=T(gaits), xref=T(np.zeros((per, 12, N + 1))),
+             fsteps=T(np.zeros((per, 20, 13))), rot=T(np.zeros(per), torch.int32), h_rot=T(np.full(per, 0.2)),
+             status=T(np.zeros(per), torch.int32), red=T(np.zeros(per), torch.int32))
+    eng = mpcq.Engine(N, device=local)
+    stream = torch.cuda.Stream(dev)
+    eng.set_stream(stream.cuda_stream)
+
+    def step(i):
+        eng.plan_device(per, mpcq.PLAN_TICK, i, d["state"].data_ptr(), d["l_feet"].data_ptr(), d["v_ref"].data_ptr(),
+                        d["gait"].data_ptr(), d["rot"].data_ptr(), d["h_rot"].data_ptr(), d["xref"].data_ptr(),
+                        d["fsteps"].data_ptr(), status_ptr=d["status"].data_ptr(), reduced_ptr=d["red"].data_ptr(),
+                        asynchronous=True)
+
+    wall, ms = _timed(torch, dist, dev, world, stream, step, args.steps, args.warmup)
+    ok = int((d["status"] == 0).sum().item())
+    if rank == 0:
+        by = model.planner_bytes_per_instance(N) * per
+        ach = by / (ms * 1e-3) / 1e9
+        out = {"metric": "FootstepPlanner instances/s (update_fsteps + getRefStates per robot)", "value":
+               per * world * args.steps / wall, "unit": "planner instances/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic robots (trot/bound/pace)",
+               "config": {"workload": f"planner tick, {per} robots per GPU, N={N}", "horizon": N,
+                          "parallelism": f"shard{world}"},
+               "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                            "frac": ach / PEAK_HBM_GBS, "traffic": load_traffic(f"plan_N{N}_B{per}"),
+                            "note": f"algorithmic {model.planner_bytes_per_instance(N)} B/robot x {per} robots "
+                                    "per launch / HIP-event launch time"},
+               "kernel_ms_per_launch": ms, "ok_fraction": ok / per}
+        if world == 1 and args.cpu_sample > 0:
+            from oracle import oracle as O
+            O.build()
+            ns = min(args.cpu_sample, per)
+            pls = [O.Planner(N, gaits[b]) for b in range(ns)]
+            t = time.perf_counter()
+            reps = 0
+            while time.perf_counter() - t < 10.0:
+                for b in range(ns):
+                    pls[b].plan(O.PLAN_TICK, reps + 1, state[b], l_feet[b], v_ref[b])
+                reps += 1
+            tc = time.perf_counter() - t
+            out["cpu_baseline"] = {"value": ns * reps / tc, "unit": "planner instances/s", "cores": 1, "kind": "port",
+                                   "sample": f"{ns} robots x {reps} ticks, oracle/planner_oracle.c through ctypes, "
+                                             f"1 thread, {tc:.1f} s"}
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main_tick(args):
+    """Closed-loop sessions: one step = one tick of every robot on this rank
+    (planner + warm-started fused solve + retrieve), virtual robot."""
+    torch, dist, world, rank, local, dev = _dist_setup()
+    import mpcq
+    from mpcq import model, synth
+    cfg = CONFIGS[args.config]
+    N = cfg["N"]
+    per = args.batch or (cfg["per_gpu"] or -(-cfg["total"] // world))
+    rng = np.random.default_rng(args.seed + rank)
+    gaits = np.stack([synth.gait_table(cfg["gaits"][b % len(cfg["gaits"])], N) for b in range(per)])
+    v_ref = np.stack([rng.uniform(-.5, 1, per), rng.uniform(-.3, .3, per), np.zeros(per), np.zeros(per),
+                      np.zeros(per), rng.uniform(-.5, .5, per)], axis=1)
+    vr = torch.from_numpy(v_ref).to(dev)
+    eng = mpcq.Engine(N, device=local)
+    stream = torch.cuda.Stream(dev)
+    eng.set_stream(stream.cuda_stream)
+    sess = mpcq.Session(eng, per, gait0=gaits)
+    warm = max(args.warmup, 1)  # tick 0 (setup, cold) is always a warm-up tick
+
+    def step(i):
+        sess.tick_device(vr.data_ptr(), k=i, asynchronous=True)
+
+    wall, ms = _timed(torch, dist, dev, world, stream, step, args.steps, warm)
+    plan_ms, solve_ms = eng.last_kernel_ms()
+    st = sess.read(mpcq.SV_STATUS)
+    it = sess.read(mpcq.SV_ITERS)
+    if rank == 0:
+        fl = model.flops(N, it, np.zeros_like(it)).sum()
+        ach = fl / (solve_ms * 1e-3) / 1e12
+        out = {"metric": "closed-loop robot ticks/s (planner + warm-started OSQP solve + retrieve per robot)",
+               "value": per * world * args.steps / wall, "unit": "robot ticks/s", "n_gpus": world,
+               "steps": args.steps, "warmup": warm, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+               "data": "synthetic robots, virtual robot closed loop (state from the previous prediction)",
+               "config": {"workload": f"session tick, {per} robots per GPU, N={N}, gaits {list(cfg['gaits'])}",
+                          "horizon": N, "parallelism": f"shard{world}"},
+               "roofline": {"bound": "mfma", "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                            "frac": ach / PEAK_FP64_TFLOPS, "traffic": None,
+                            "note": "engine kernel of the last tick: model.flops(measured iterations, rho updates "
+                                    "taken as 0 -- a lower bound) / its HIP-event time"},
+               "kernel_ms": {"step": ms, "planner_last_tick": plan_ms, "solve_last_tick": solve_ms},
+               "solved_fraction": float(np.isin(st, (1, 2)).mean()),
+               "iters_warm": {"median": float(np.median(it)), "p90": float(np.percentile(it, 90)),
+                              "max": int(it.max())}}
+        if world == 1 and args.cpu_sample > 0:
+            from oracle import oracle as O
+            O.build()
+            ns = min(16, per)
+            ors = [O.Session(N, gaits[b]) for b in range(ns)]
+            t = time.perf_counter()
+            ticks = 0
+            while time.perf_counter() - t < 10.0 and ticks < 200:
+                for b in range(ns):
+                    ors[b].tick(ticks, v_ref[b])
+                ticks += 1
+            tc = time.perf_counter() - t
+            out["cpu_baseline"] = {"value": ns * ticks / tc, "unit": "robot ticks/s", "cores": 1, "kind": "port",
+                                   "sample": f"{ns} robots x {ticks} ticks of oracle.Session (C restatements via "
+                                             f"ctypes), 1 thread, {tc:.1f} s"}
+        print(json.dumps(out), flush=True)
+    sess.close()
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.mode == "plan":
+        return main_plan(args)
+    if args.mode == "tick":
+        return main_tick(args)
     import torch
     import torch.distributed as dist
 

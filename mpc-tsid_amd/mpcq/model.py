@@ -53,3 +53,22 @@ def flops(N: int, iters, rho_updates, check_every: int = 25, adapt_every: int = 
         n_checks += np.floor(K / adapt_every) - np.floor(K / np.lcm(check_every, adapt_every))
     n_checks += 1  # final evaluation when the loop exits on max_iter without a check
     return c["form"] + c["scale"] + (1 + R) * c["fact"] + K * c["iter"] + n_checks * c["check"]
+
+
+def planner_bytes_per_instance(N: int, with_reduced: bool = True) -> int:
+    """Compulsory HBM bytes of one MPCQ_PLAN_TICK planner instance: reads gait,
+    state, l_feet, v_ref, (reduced), rotation flag / height and xref (in/out);
+    writes gait, xref, fsteps, rotation flag / height and status."""
+    nx = 8 * 12 * (N + 1)
+    rd = 800 + 96 + 96 + 48 + (4 if with_reduced else 0) + 4 + 8 + nx
+    wr = 800 + nx + 8 * 260 + 4 + 8 + 4
+    return rd + wr
+
+
+def retrieve_bytes_per_instance(N: int) -> int:
+    """Compulsory HBM bytes of the session epilogue: reads x, xref, status, plan
+    status, fsteps rows 0-1, gait row 0, q_w; writes x_robot, warm_x, cost, q_w,
+    next state and feet."""
+    rd = 8 * 24 * N + 8 * 12 * (N + 1) + 4 + 4 + 8 * 26 + 8 + 48
+    wr = 8 * 12 * N + 8 * 24 * N + 8 * 13 + 48 + 96 + 96
+    return rd + wr

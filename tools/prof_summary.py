@@ -26,12 +26,12 @@ import shutil
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def counters(path):
+def counters(path, kernel="engine_kernel"):
     agg = collections.defaultdict(list)
     if not os.path.exists(path):
         return agg
     for r in csv.DictReader(open(path)):
-        if "engine_kernel" in r["Kernel_Name"]:
+        if kernel in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     return agg
 
@@ -45,6 +45,7 @@ def main():
     ap.add_argument("tag")
     ap.add_argument("--key", default="c2_N16_B1024")
     ap.add_argument("--instances", type=int, default=1024)
+    ap.add_argument("--kernel", default="engine_kernel", help="substring of the kernel the counters describe")
     a = ap.parse_args()
     src = os.path.join(REPO, "gpurun_out", f"prof_{a.tag}")
     dst = os.path.join(REPO, "profiles")
@@ -52,13 +53,14 @@ def main():
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{a.tag}_kernel_stats.csv"))
 
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
-    eng = [r for r in stats if "engine_kernel" in r["Name"]]
+    eng = [r for r in stats if a.kernel in r["Name"]]
+    others = [r for r in stats if a.kernel not in r["Name"]]
     trace = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
-             if "engine_kernel" in r["Kernel_Name"]]
-    fetch = counters(os.path.join(src, "fetch", "run_counter_collection.csv"))
-    write = counters(os.path.join(src, "write", "run_counter_collection.csv"))
-    sq = counters(os.path.join(src, "sq", "run_counter_collection.csv"))
-    for k2, v2 in counters(os.path.join(src, "sq2", "run_counter_collection.csv")).items():
+             if a.kernel in r["Kernel_Name"]]
+    fetch = counters(os.path.join(src, "fetch", "run_counter_collection.csv"), a.kernel)
+    write = counters(os.path.join(src, "write", "run_counter_collection.csv"), a.kernel)
+    sq = counters(os.path.join(src, "sq", "run_counter_collection.csv"), a.kernel)
+    for k2, v2 in counters(os.path.join(src, "sq2", "run_counter_collection.csv"), a.kernel).items():
         if k2 != "SQ_WAVES":
             sq[k2] = v2
 
@@ -68,6 +70,9 @@ def main():
     for r in eng:
         lines.append(f"- kernel `{r['Name']}`: {r['Calls']} calls, average {float(r['AverageNs']) / 1e6:.3f} ms "
                      f"(min {float(r['MinNs']) / 1e6:.3f}, max {float(r['MaxNs']) / 1e6:.3f}), "
+                     f"{r['Percentage']} % of GPU time")
+    for r in others:
+        lines.append(f"- (other) `{r['Name'][:90]}`: {r['Calls']} calls, average {float(r['AverageNs']) / 1e3:.1f} us, "
                      f"{r['Percentage']} % of GPU time")
     if trace:
         t = trace[0]

@@ -27,7 +27,10 @@ struct PlanShared {
   double gait[100];
   double fs[260];
   double v6[33], v7[33];
-  int bad;
+  // the instance's small inputs: state 0..11, v_ref 12..17, v_cur 18..23,
+  // l_feet 24..35, h 36, h_rot 37
+  double in[38];
+  int flag, reduced, bad;
 };
 
 // numpy.linspace(a, b, n)[i] with endpoint: i * ((b - a) / (n - 1)) + a, last = b
@@ -44,12 +47,33 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
   if (b >= a.batch) return;
   const int N = a.N, NP = a.N + 1;
   double* gg = a.gait + b * 100;
-  const double* st = a.state + b * 12;
-  const double* vr = a.v_ref + b * 6;
+  double* gx = a.xref + b * 12 * NP;
+  const bool do_ref = a.ops & MPCQ_PLAN_REFSTATES, do_fs = a.ops & MPCQ_PLAN_FOOTSTEPS;
 
-  for (int e = lane; e < 100; e += 64) sh.gait[e] = gg[e];
-  if (lane == 0) sh.bad = 0;
+  // Every global read of the instance is issued here, before the first
+  // barrier, so the wave pays one memory latency instead of one per phase.
+  const double g0 = gg[lane];
+  const double g1 = lane < 36 ? gg[64 + lane] : 0.0;
+  double x[12];  // xref column `lane` (getRefStates rewrites only some rows)
+  const bool col = do_ref && lane < NP;
+#pragma unroll
+  for (int r = 0; r < 12; ++r) x[r] = col ? gx[r * NP + lane] : 0.0;
+  double iv = 0.0;
+  if (lane < 12) iv = a.state[b * 12 + lane];
+  else if (lane < 18) iv = a.v_ref[b * 6 + lane - 12];
+  else if (lane < 24) iv = a.v_cur ? a.v_cur[b * 6 + lane - 18] : a.state[b * 12 + lane - 12];
+  else if (lane < 36) iv = do_fs ? a.l_feet[b * 12 + lane - 24] : 0.0;
+  else if (lane == 36) iv = a.h ? a.h[b] : a.state[b * 12 + 2];
+  else if (lane == 37) iv = do_ref ? a.h_rot[b] : 0.0;
+  if (lane == 38) sh.flag = do_ref ? a.rot_flag[b] : 0;
+  if (lane == 39) sh.reduced = a.reduced ? a.reduced[b] : 0;
+  if (lane == 40) sh.bad = 0;
+  sh.gait[lane] = g0;
+  if (lane < 36) sh.gait[64 + lane] = g1;
+  if (lane < 38) sh.in[lane] = iv;
   __syncthreads();
+  const double* st = sh.in;
+  const double* vr = sh.in + 12;
 
   // ---- roll (FootstepPlanner.py:401-425)
   if (a.ops & MPCQ_PLAN_ROLL) {
@@ -103,9 +127,9 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
 
   // ---- compute_footsteps (FootstepPlanner.py:284-361)
   if (a.ops & MPCQ_PLAN_FOOTSTEPS) {
-    const double* vc = a.v_cur ? a.v_cur + b * 6 : st + 6;
-    const double h = a.h ? a.h[b] : st[2];
-    const int reduced = a.reduced ? a.reduced[b] : 0;
+    const double* vc = sh.in + 18;
+    const double h = sh.in[36];
+    const int reduced = sh.reduced;
     for (int e = lane; e < 260; e += 64) sh.fs[e] = (e % 13 == 0) ? sh.gait[5 * (e / 13)] : NAN;
     __syncthreads();
     if (lane < 12) {
@@ -131,7 +155,7 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
         }
       }
       // row 0: stance feet where they are (l_feet.ravel('F')[c] = l_feet[r][q])
-      const double l0 = sh.gait[1 + q] == 1.0 ? a.l_feet[b * 12 + 4 * r + q] : NAN;
+      const double l0 = sh.gait[1 + q] == 1.0 ? sh.in[24 + 4 * r + q] : NAN;
       double prev = l0;  // fsteps[i-1, 1+c]
       sh.fs[1 + c] = l0;
       bool prev_st = sh.gait[1 + q] == 1.0;
@@ -176,12 +200,7 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
 
   // ---- getRefStates (FootstepPlanner.py:76-159)
   if (a.ops & MPCQ_PLAN_REFSTATES) {
-    double* gx = a.xref + b * 12 * NP;
     const int j = lane;
-    const bool col = j < NP;
-    double x[12];
-#pragma unroll
-    for (int r = 0; r < 12; ++r) x[r] = col ? gx[r * NP + j] : 0.0;
     const double Tg = pp.T_gait, dt = pp.dt;
     if (col && j >= 1) {
       const double yaw = linspace_at(0.0, Tg - dt, N, j - 1) * vr[5];
@@ -209,8 +228,8 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
       for (int r = 0; r < 12; ++r) x[r] = st[r];
     }
     // height / rotation command state machine (uniform per instance)
-    int flag = a.rot_flag[b];
-    double h_rot = a.h_rot[b];
+    int flag = sh.flag;
+    double h_rot = sh.in[37];
     const double step = pp.cmd_threshold;
     const double v2 = vr[2];
     if (fabs(v2) > step && flag != 1) flag = 1;

@@ -141,7 +141,18 @@ class MPC:
 
 
 class MPC_Wrapper:
-    """MPC_Wrapper.py:20-112 over the HIP engine (synchronous)."""
+    """MPC_Wrapper.py:20-290 over the HIP engine.
+
+    ``multiprocessing=False``: ``solve`` runs the tick and returns when it is
+    done (MPC_Wrapper.py:83-112).  ``multiprocessing=True``: the asynchronous
+    contract the reference sketches with a worker process and shared memory
+    (MPC_Wrapper.py:116-215, which its ``solve`` currently refuses to run):
+    ``solve`` snapshots the planner's xref / fsteps (replacing NaN by 0 in the
+    caller's fsteps, as compress_dataIn does, MPC_Wrapper.py:222) and returns at
+    once while the tick runs on a worker thread (the HIP call releases the GIL);
+    ``get_latest_result`` hands back that tick's forces once (newResult,
+    MPC_Wrapper.py:69-74), waiting for it if it is still running, and raises the
+    reference's ValueError when no tick was submitted since the last result."""
 
     def __init__(self, dt, n_steps, k_mpc, T_gait, multiprocessing=False, device: int = 0,
                  engine: Engine | None = None, **overrides):
@@ -150,13 +161,35 @@ class MPC_Wrapper:
         self.k_mpc = k_mpc
         self.multiprocessing = multiprocessing
         self.mpc = MPC(dt, n_steps, T_gait, device=device, engine=engine, **overrides)
+        self._pool = None
+        self._pending = None
+        if multiprocessing:
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="mpcq-async")
 
     def solve(self, k, fstep_planner):
         if self.multiprocessing:
-            # the reference raises here too (MPC_Wrapper.py:48-50)
-            raise RuntimeError("Error: Asynchronous MPC is not up to date")
-        self.run_MPC_synchronous(k, fstep_planner)
+            self.run_MPC_asynchronous(k, fstep_planner)
+        else:
+            self.run_MPC_synchronous(k, fstep_planner)
         return 0
+
+    def run_MPC_asynchronous(self, k, fstep_planner):
+        fs = fstep_planner.fsteps
+        fs[np.isnan(fs)] = 0.0  # MPC_Wrapper.py:222
+        xref, fsteps = np.array(fstep_planner.xref, copy=True), np.array(fs, copy=True)
+
+        def job():
+            self.mpc.run(k / self.k_mpc, xref, fsteps)
+            return self.mpc.f_applied.copy()
+
+        self._pending = self._pool.submit(job)
+        return 0
+
+    def close(self):
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+            self._pool = None
 
     def run_MPC_synchronous(self, k, fstep_planner):
         self.mpc.run(k / self.k_mpc, fstep_planner.xref, fstep_planner.fsteps)
@@ -176,6 +209,12 @@ class MPC_Wrapper:
 
     def get_latest_result(self):
         if self.not_first_iter:
+            if self.multiprocessing:
+                if self._pending is None:
+                    raise ValueError("Error: something went wrong with the MPC, result not available.")
+                fut, self._pending = self._pending, None
+                self.f_applied = fut.result()
+                return self.f_applied
             return self.mpc.f_applied
         self.not_first_iter = True
         return np.array([0.0, 0.0, 8.0] * 4)

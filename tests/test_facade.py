@@ -69,11 +69,45 @@ def test_run_mpc_alias_and_virtual(oracle, golden16):
 
 def test_errors(oracle, golden16):
     from mpcq.wrapper import MPC_Wrapper
+    # asynchronous: the tick's error surfaces where its result is collected
     w = MPC_Wrapper(0.02, 16, 20, 0.32, multiprocessing=True, engine=OracleEngine(oracle))
-    with pytest.raises(RuntimeError):
-        w.solve(0, Planner(golden16["xref"][0], golden16["fsteps"][0]))
+    w.get_latest_result()
+    w.solve(0, Planner(golden16["xref"][0], golden16["bad_fsteps"][0]))
+    with pytest.raises(ValueError):
+        w.get_latest_result()
+    w.close()
     w = MPC_Wrapper(0.02, 16, 20, 0.32, engine=OracleEngine(oracle))
     with pytest.raises(ValueError):
         w.solve(0, Planner(golden16["xref"][0], golden16["bad_fsteps"][0]))
     with pytest.raises(ValueError):
         w.solve(0, Planner(golden16["xref"][0][:, :5], golden16["fsteps"][0]))
+
+
+def test_async_wrapper_contract(oracle, golden16):
+    """multiprocessing=True: solve returns at once, get_latest_result hands each
+    tick's forces back once (MPC_Wrapper.py:64-78, 116-215)."""
+    from mpcq.wrapper import MPC_Wrapper
+    w = MPC_Wrapper(0.02, 16, 20, 0.32, multiprocessing=True, engine=OracleEngine(oracle))
+    s = MPC_Wrapper(0.02, 16, 20, 0.32, engine=OracleEngine(oracle))
+    assert w.get_latest_result().tolist() == [0.0, 0.0, 8.0] * 4
+    s.get_latest_result()
+    with pytest.raises(ValueError):
+        w.get_latest_result()  # nothing submitted
+    for tick in range(3):
+        pl = Planner(golden16["xref"][tick], golden16["fsteps"][tick])
+        pl2 = Planner(golden16["xref"][tick], golden16["fsteps"][tick])
+        assert w.solve(20 * tick, pl) == 0
+        assert not np.isnan(pl.fsteps).any()  # compress_dataIn's NaN -> 0 (MPC_Wrapper.py:222)
+        s.solve(20 * tick, pl2)
+        assert np.array_equal(w.get_latest_result(), s.get_latest_result())
+        with pytest.raises(ValueError):
+            w.get_latest_result()  # consumed
+    w.close()
+
+
+def test_footstep_planner_facade_errors_without_device():
+    """The planner façade has no CPU fallback: without a HIP device it raises."""
+    import mpcq
+    from mpcq.planner import FootstepPlanner
+    with pytest.raises(mpcq.MpcqError):
+        FootstepPlanner(0.02, 1)

@@ -34,3 +34,55 @@ def test_solve_batch(golden16, oracle):
     ref = oracle.solve_batch(golden16["xref"][:8], golden16["fsteps"][:8], 0, nthreads=4)
     assert np.array_equal(info["status"], ref["status"])
     assert np.abs(f0 - ref["f0"]).max() < 1e-6
+
+
+def test_footstep_planner_facade_vs_reference_fixtures():
+    """The drop-in FootstepPlanner (one robot on the GPU) driven exactly as the
+    reference control loop drives the reference class (processing.py:80-131)
+    reproduces the captured reference states (tests/golden/planner_golden.npz)."""
+    import os
+    from mpcq.planner import FootstepPlanner
+    G = np.load(os.path.join(os.path.dirname(__file__), "golden", "planner_golden.npz"))
+    for N, n_periods in ((16, 1), (32, 2)):
+        for s in range(G[f"n{N}_state"].shape[0]):
+            pl = FootstepPlanner(0.02, n_periods)
+            if str(G[f"n{N}_kind"][s]) != "trot":
+                pl.gait = G[f"n{N}_gait0"][s].copy()
+            assert np.array_equal(pl.gait, G[f"n{N}_gait0"][s])
+            for j in range(6):
+                st = G[f"n{N}_state"][s, j]
+                lC, abg, lV, lW = st[0:3, None], st[3:6, None], st[6:9, None], st[9:12, None]
+                lf, vr, red = G[f"n{N}_l_feet"][s, j], G[f"n{N}_v_ref"][s, j][:, None], bool(G[f"n{N}_reduced"][s, j])
+                v_cur = np.vstack((lV, lW))
+                if j == 0:
+                    pl.update_fsteps(0, lf, v_cur, vr, lC[2, 0], None, None, red)
+                pl.update_fsteps(j * 20 + 1, lf, v_cur, vr, lC[2, 0], None, None, red)
+                pl.getRefStates(float(j), pl.T_gait, lC, abg, lV, lW, vr, h_ref=0.2027682)
+                assert np.array_equal(pl.gait, G[f"n{N}_gait"][s, j]), (N, s, j)
+                assert pl.flag_rotation_command == G[f"n{N}_flag"][s, j]
+                assert np.array_equal(np.isnan(pl.fsteps), np.isnan(G[f"n{N}_fsteps"][s, j]))
+                assert np.nanmax(np.abs(pl.fsteps - G[f"n{N}_fsteps"][s, j])) <= 1e-15
+                assert np.abs(pl.xref - G[f"n{N}_xref"][s, j]).max() <= 1e-15
+            pl.engine.close()
+    bad = FootstepPlanner(0.02, 1)
+    bad.gait = G["bad_gait"].copy()
+    with pytest.raises(TypeError):
+        bad.roll()
+    with pytest.raises(IndexError):
+        bad.compute_footsteps(np.zeros((3, 4)), np.zeros((6, 1)), np.zeros((6, 1)), 0.2, False)
+
+
+def test_async_wrapper_matches_sync(golden16):
+    """multiprocessing=True on the GPU: the worker-thread tick returns what the
+    synchronous wrapper returns."""
+    from mpcq.wrapper import MPC_Wrapper
+    wa = MPC_Wrapper(0.02, 16, 20, 0.32, multiprocessing=True, device=0)
+    ws = MPC_Wrapper(0.02, 16, 20, 0.32, device=0)
+    wa.get_latest_result()
+    ws.get_latest_result()
+    for tick in range(4):
+        b = tick % 3
+        wa.solve(20 * tick, Planner(golden16["xref"][b], golden16["fsteps"][b]))
+        ws.solve(20 * tick, Planner(golden16["xref"][b], golden16["fsteps"][b]))
+        assert np.array_equal(wa.get_latest_result(), ws.get_latest_result())
+    wa.close()

@@ -72,9 +72,9 @@ int check_params(const mpcq_params* p) {
   if (!(p->force_weight > 0)) return fail(MPCQ_E_INVALID, "force_weight must be > 0");
   for (int i = 0; i < 12; ++i)
     if (!(p->state_weights[i] > 0)) return fail(MPCQ_E_INVALID, "state weights must be > 0");
-  if (p->polish != 0)
-    return fail(MPCQ_E_UNSUPPORTED, "polish is not implemented in the HIP engine yet (polish must be 0, "
-                                    "the OSQP default the reference runs with)");
+  if (p->polish < 0 || p->polish > 2) return fail(MPCQ_E_INVALID, "polish must be 0, 1 or 2");
+  if (p->polish && (!(p->delta > 0) || p->polish_refine_iter < 0 || p->polish_rounds < 1))
+    return fail(MPCQ_E_INVALID, "polish needs delta > 0, polish_refine_iter >= 0, polish_rounds >= 1");
   return MPCQ_OK;
 }
 

@@ -255,6 +255,9 @@ __device__ __forceinline__ double sel3(int i, double a0, double a1, double a2) {
 template <int PV>
 __device__ __forceinline__ void gj_step(double (&R)[12], int me, bool& ok) {
   const double d = rbc<LN(PV)>(R[PV]);
+#ifdef MPCQ_DEBUG_PIVOT
+  if (!(d > 0.0) && me == PV) printf("pivot fail blk %d thr %d PV %d d %g\n", (int)blockIdx.x, (int)threadIdx.x, PV, d);
+#endif
   if (!(d > 0.0)) ok = false;
   const double id = 1.0 / d;
   const double mrp = R[PV];
@@ -402,7 +405,7 @@ struct Prologue {
 // The engine kernel.  FUSED: formulate from (xref, fsteps) then solve.
 // !FUSED: solve the given (Ax, l, u).  SOLVE=false: formulation only.
 
-template <int N, bool FUSED, bool SOLVE>
+template <int N, bool FUSED, bool SOLVE, bool POLISH>
 __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, LaunchArgs a) {
   constexpr int NW = N / 4, T = 16 * N, n = 24 * N, m = 44 * N, nnz = 126 * N - 18, MID = N / 2;
   __shared__ Smem<N> sh;
@@ -616,7 +619,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     for (int j = 0; j < 12; ++j) Fr[j] = 0.0;
     unsigned cls = 0u;
     double cscale = 1.0;
-    int it_done = 0, n_upd = 0;
+    int it_done = 0, n_upd = 0, pol_st = 0, pol_rounds = 0;
 #ifdef MPCQ_FACTIME
     uint64_t fac_cycles = 0;
 #endif
@@ -638,7 +641,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         ri[j] = cj == RC_EQ ? ri_eq : (cj == RC_INEQ ? ri_in : 1.0 / kRhoMin);
       }
     };
-    auto rho_of = [&](int j) __attribute__((always_inline)) -> double {
+    auto rho_of_cls = [&](int j) __attribute__((always_inline)) -> double {
       const unsigned cj = (cls >> (2 * j)) & 3u;
       return cj == RC_EQ ? r_eq : (cj == RC_INEQ ? r_in : kRhoMin);
     };
@@ -750,9 +753,14 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       }
     };
 
-    auto factor = [&](double sigma) __attribute__((always_inline)) -> bool {
+    // pr: per-own-row rho override (polish: 1/delta on active rows, 0 elsewhere);
+    // nullptr in the ADMM loop, where the class rho applies
+    auto factor = [&](double sigma, const double* pr) __attribute__((always_inline)) -> bool {
       bool ok = true;
       launder();
+      auto rho_of = [&](int j) __attribute__((always_inline)) -> double {
+        return pr ? pr[j] : rho_of_cls(j);
+      };
       double* gk = sh.GH[k];
       if (cl) gk[108 + ph] = rho_of(0);
       sync_all();
@@ -1223,32 +1231,13 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       sync_all();
       STAMP(1);
 
-      // ------------------------------------------------------------ ADMM
-      // The factorisation sits outside the hot loop: the outer loop factors,
-      // the inner loop iterates until convergence, max_iter or a rho update.
-      bool last_checked = false;
-      int iter = 1;
-      int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
-      double lo[3], hi[3];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) { lo[j] = lo_of(j); hi[j] = hi_of(j); }
-      for (;;) {
-#ifndef MPCQ_REP_FACTOR
-#define MPCQ_REP_FACTOR 1
-#endif
-        bool fac_ok = true;
-#ifdef MPCQ_FACTIME
-        const uint64_t ft0_ = __builtin_amdgcn_s_memtime();
-#endif
-#pragma nounroll
-        for (int rep_ = 0; rep_ < MPCQ_REP_FACTOR; ++rep_) fac_ok = factor(p.sigma);  // > 1: timing only
-#ifdef MPCQ_FACTIME
-        fac_cycles += __builtin_amdgcn_s_memtime() - ft0_;
-#endif
-        if (!fac_ok) { status = MPCQ_STATUS_FACTOR_FAILED; break; }
-        STAMP(2);
-        bool refactor = false;
-        for (; iter <= p.max_iter; ++iter) {
+      // The phases of one KKT solve (K w = b, K = P + sigma I + A'RA as factored):
+      // ph_rhs publishes the sweep right-hand sides of b = xc + A' w (P1-P4), ph_sweep
+      // runs the state sweeps (P5-P7), ph_recover the forces and A w on the own rows
+      // (P8, P9's first half).  The ADMM loop calls them with admm = true (w = rho z - y,
+      // xc = sigma x); polish with its own w and x terms.
+      auto ph_rhs = [&](bool admm, const double (&pw)[3], double xcf, double xcX, double& uf,
+                        double& beta) __attribute__((always_inline)) {
           launder_p();
           // P1-P4: w = rho z - y; b_f = sigma x_f + A_f' w and u = F b_f, beta = R B u
           // (stage-local, DPP only); then the sweep right-hand side of the own state
@@ -1264,16 +1253,16 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           const double cXd = Ab[oXd], cHd = Ab[oHdm], cH6 = Ab[oH6m];
           double w[3];
 #pragma unroll
-          for (int j = 0; j < 3; ++j) w[j] = rr[j] * z[j] - y[j];
+          for (int j = 0; j < 3; ++j) w[j] = admm ? rr[j] * z[j] - y[j] : pw[j];
           // the phase's arithmetic starts after this point, the loads before it
           asm volatile("" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]) : : "memory");
-          const double bf = colF_c(cf, w) + p.sigma * xf;  // b_f = sigma x_f + A_f' w (- q, q = 0)
+          const double bf = colF_c(cf, w) + (admm ? p.sigma * xf : xcf);  // b_f = sigma x_f + A_f' w (- q, q = 0)
           // u = F b_f (kept for the forces) and beta = R B u = (F W)' b_f (rows 6..11)
-          const double uf = bdot_ln12(Fr, bf, 0.0);
-          const double beta = bdot_ln12(fwc, bf, 0.0);
+          uf = bdot_ln12(Fr, bf, 0.0);
+          beta = bdot_ln12(fwc, bf, 0.0);
           {
             const double wd = w[0] - beta;  // dynamics-row w less the force Schur term (beta = 0 on rows 0..5)
-            const double bo = p.sigma * xX + cXd * wd;
+            const double bo = (admm ? p.sigma * xX : xcX) + cXd * wd;
             const double na = cHd * wd;                  // Hd(k, ph): on X_k[ph], stage k-1's column ph
             const double nb = cH6 * w[0];                // H6(k, ph): on X_k[ph+6] (ph < 6)
             // stage 0 zeroes the last stage's na / nb (that stage has no next stage:
@@ -1284,6 +1273,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           }
           sync_all();
           STAMP(3);
+      };
+      auto ph_sweep = [&]() __attribute__((always_inline)) {
           // P5-P7: the state solve on wave 0 alone (no block barrier inside).
           // Inward step j = 1..MID: top kk(j) = j, bottom kk(j) = N-1-j.  Half 0 (rows
           // 0 top / 1 bottom) runs the recurrence y_kk = b_kk - G_kk y_kk(j-1) (G_kk of
@@ -1411,9 +1402,12 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           }  // MPCQ_REP_SWEEP
           sync_all();
           STAMP(7);
+      };
+      auto ph_recover = [&](double uf, double beta, double& sf, double& sX, double (&ax)[3])
+          __attribute__((always_inline)) {
           // P8: forces f_k = F_k (b_f - R B' g) = u - (F W) g, with g = Xd X_{k+1} + Hd X_k
           // on the velocity rows (the states' part of those rows)
-          double sf, sX, gv;
+          double gv;
           // all LDS operands of P8 / P9 first (one round trip)
           const double xa = XSr[oXSp], xb = XSr[oXSp6];
           sX = XSr[oXS];
@@ -1431,7 +1425,6 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           // P9: z, y update (osqp update_z / update_y), x update.  A x~ on the own rows:
           // dynamics rows use B f = B u - B F W g = beta / rho - (R^{-1} Q) g (no force gather)
           {
-            double ax[3];
             {
               // B f on the velocity rows (zero coefficients elsewhere)
               const double bfv = beta * ri[0] - bdot_ln6v(qll, gv, 0.0);
@@ -1445,6 +1438,42 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               ax[1] = cl ? swg : frB;
               ax[2] = cl ? frA : 0.0;
             }
+          }
+      };
+      const double kNoW[3] = {0.0, 0.0, 0.0};
+
+      // ------------------------------------------------------------ ADMM
+      // The factorisation sits outside the hot loop: the outer loop factors,
+      // the inner loop iterates until convergence, max_iter or a rho update.
+      bool last_checked = false;
+      int iter = 1;
+      int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
+      double lo[3], hi[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) { lo[j] = lo_of(j); hi[j] = hi_of(j); }
+      for (;;) {
+#ifndef MPCQ_REP_FACTOR
+#define MPCQ_REP_FACTOR 1
+#endif
+        bool fac_ok = true;
+#ifdef MPCQ_FACTIME
+        const uint64_t ft0_ = __builtin_amdgcn_s_memtime();
+#endif
+#pragma nounroll
+        for (int rep_ = 0; rep_ < MPCQ_REP_FACTOR; ++rep_) fac_ok = factor(p.sigma, nullptr);  // > 1: timing only
+#ifdef MPCQ_FACTIME
+        fac_cycles += __builtin_amdgcn_s_memtime() - ft0_;
+#endif
+        if (!fac_ok) { status = MPCQ_STATUS_FACTOR_FAILED; break; }
+        STAMP(2);
+        bool refactor = false;
+        for (; iter <= p.max_iter; ++iter) {
+          double uf, beta, sf, sX, ax[3];
+          ph_rhs(true, kNoW, 0.0, 0.0, uf, beta);
+          ph_sweep();
+          ph_recover(uf, beta, sf, sX, ax);
+          // P9: z, y update (osqp update_z / update_y), x update
+          {
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
               const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
@@ -1494,6 +1523,174 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         if (status == 0)
           status = converged(10.0) ? MPCQ_STATUS_SOLVED_INACCURATE : MPCQ_STATUS_MAX_ITER_REACHED;
       }
+
+      // ------------------------------------------------------------ polish
+      // OSQP 0.6 polish (polish.c): guess the active set from (z, y), solve the
+      // equality-constrained QP  min 1/2 x'Px  s.t. A_act x = b_act,  project
+      // (A x, y) onto the normal cone and keep the point if it lowers the
+      // residuals; polish_rounds > 1 repeats the guess from the polished point
+      // until the set repeats (primal-dual active set).  The equality QP is solved
+      // by the method of multipliers on the engine's own factorisation
+      // (K = P + sigma I + rho_p A_act' A_act, rho_p = kPolishRho):
+      //   x+ = K^{-1} (sigma x + A_act' (rho_p b - y)),  y+ = y + rho_p (A_act x+ - b),
+      // 1 + max(polish_refine_iter, kPolishMinIter) solves.  OSQP's own reduced KKT
+      // (rho = 1/delta = 1e6) is not used: the engine's stage elimination forms
+      // F = K_ff^{-1} explicitly, and at 1e6 its Schur complements lose positive
+      // definiteness (measured: negative pivots on every instance).  Equality rows
+      // stay in the set even when y is exactly 0.
+      if constexpr (POLISH) {
+        if (p.polish != 0 && (status == MPCQ_STATUS_SOLVED ||
+                              (p.polish >= 2 && (status == MPCQ_STATUS_SOLVED_INACCURATE ||
+                                                 status == MPCQ_STATUS_MAX_ITER_REACHED)))) {
+          constexpr double kPolishRho = 1e3;
+          constexpr int kPolishMinIter = 10;
+          const double a_pri = pri_res, a_dua = dua_res;
+          const double axf = xf, axX = xX;
+          double az[3], ay[3], zs[3], ys[3], bred[3], prho[3];
+          int act[3], prv[3];
+#pragma unroll
+          for (int j = 0; j < 3; ++j) { az[j] = z[j]; ay[j] = y[j]; zs[j] = z[j]; ys[j] = y[j]; prv[j] = 0; }
+          bool have = false;
+          double b_pri = 0.0, b_dua = 0.0, b_epri = 0.0, b_edua = 0.0, bxf = 0.0, bxX = 0.0, bz[3], by[3];
+          const int rounds = p.polish_rounds > 0 ? p.polish_rounds : 1;
+          const int mom = p.polish_refine_iter > kPolishMinIter ? p.polish_refine_iter : kPolishMinIter;
+          for (int rd = 0; rd < rounds; ++rd) {
+            int changed = 0;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              const int r = nat_row(j);
+              const bool eq = ((cls >> (2 * j)) & 3u) == RC_EQ;
+              int a_ = 0;
+              if (r >= 0) {
+                if (rd == 0) {  // OSQP's guess (polish.c form_Ared)
+                  if (zs[j] - lo[j] < -ys[j]) a_ = -1;
+                  else if (hi[j] - zs[j] < ys[j]) a_ = 1;
+                  if (eq && a_ == 0) a_ = 1;
+                } else {  // keep correctly signed active rows, add violated rows
+                  const double tol = 1e-12;
+                  if (prv[j] == -1 && (ys[j] <= tol || eq)) a_ = -1;
+                  else if (prv[j] == 1 && (ys[j] >= -tol || eq)) a_ = 1;
+                  else if (zs[j] < lo[j] - tol) a_ = -1;
+                  else if (zs[j] > hi[j] + tol) a_ = 1;
+                }
+              }
+              changed |= a_ != prv[j];
+              act[j] = a_;
+              prv[j] = a_;
+              bred[j] = a_ < 0 ? lo[j] : (a_ > 0 ? hi[j] : 0.0);
+              prho[j] = a_ ? kPolishRho : 0.0;
+            }
+            if (rd > 0) {  // stop when the set repeats (uniform over the block)
+              if (t == 0) sh.flag[3] = 0;
+              sync_all();
+              if (changed) atomicOr(&sh.flag[3], 1);
+              sync_all();
+              const bool same = sh.flag[3] == 0;
+              sync_all();
+              if (same) break;
+            }
+            ++pol_rounds;
+            if (!factor(p.sigma, prho)) break;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) { rr[j] = prho[j]; ri[j] = act[j] ? 1.0 / kPolishRho : 0.0; }
+            // one proximal multiplier step from the ADMM point (x, y on the active rows),
+            // then refinement against the true residuals of the equality QP
+            //   r_x = -(P x + A_act' y),  r_y = b - A_act x,
+            //   dx = K^{-1} (r_x + rho_p A_act' r_y),  dy = rho_p (A_act dx - r_y),
+            // so that the error of the explicit stage inverses does not reach the fixed point
+            double xpf, xpX, axp[3], yp[3];
+            {
+              double pw[3], uf, beta, ax[3];
+#pragma unroll
+              for (int j = 0; j < 3; ++j) {
+                yp[j] = act[j] ? y[j] : 0.0;
+                pw[j] = act[j] ? kPolishRho * bred[j] - yp[j] : 0.0;
+              }
+              ph_rhs(false, pw, p.sigma * xf, p.sigma * xX, uf, beta);
+              ph_sweep();
+              ph_recover(uf, beta, xpf, xpX, ax);
+#pragma unroll
+              for (int j = 0; j < 3; ++j) {
+                axp[j] = ax[j];
+                if (act[j]) yp[j] += kPolishRho * (ax[j] - bred[j]);
+              }
+            }
+            for (int it_ = 0; it_ < mom; ++it_) {
+              double pw[3], ry[3], uf, beta, dxf, dxX, ax[3];
+#pragma unroll
+              for (int j = 0; j < 3; ++j) {
+                ry[j] = act[j] ? bred[j] - axp[j] : 0.0;
+                pw[j] = act[j] ? kPolishRho * ry[j] - yp[j] : 0.0;
+              }
+              ph_rhs(false, pw, -Pbf() * xpf, -PbX() * xpX, uf, beta);
+              ph_sweep();
+              ph_recover(uf, beta, dxf, dxX, ax);
+              xpf += dxf;
+              xpX += dxX;
+#pragma unroll
+              for (int j = 0; j < 3; ++j) {
+                axp[j] += ax[j];
+                if (act[j]) yp[j] += kPolishRho * (ax[j] - ry[j]);
+              }
+#ifdef MPCQ_DEBUG_POLISH
+              {
+                double rmax = 0.0, dxm = fmax(fabs(dxf), fabs(dxX));
+                for (int j = 0; j < 3; ++j) if (act[j]) rmax = fmax(rmax, fabs(axp[j] - bred[j]));
+                for (int o = 32; o > 0; o >>= 1) { rmax = fmax(rmax, __shfl_xor(rmax, o)); dxm = fmax(dxm, __shfl_xor(dxm, o)); }
+                if (b == 0 && lane == 0) printf("blk0 wave %d rd %d it %d max|Ax-b| %.3e max|dx| %.3e\n", wv, rd, it_, rmax, dxm);
+              }
+#endif
+            }
+            // the next round guesses from the unprojected point
+#pragma unroll
+            for (int j = 0; j < 3; ++j) { zs[j] = axp[j]; ys[j] = yp[j]; }
+            // project onto the normal cone (polish.c project_normalcone), residuals
+            xf = xpf;
+            xX = xpX;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              const double tt = axp[j] + yp[j];
+              const double zz = fmin(fmax(tt, lo[j]), hi[j]);
+              z[j] = zz;
+              y[j] = tt - zz;
+            }
+#ifdef MPCQ_DEBUG_POLISH
+            if (b == 0)
+              for (int j = 0; j < 3; ++j)
+                if (fabs(y[j] - yp[j]) > 1e-9 || (act[j] == 0 && fabs(axp[j] - z[j]) > 1e-12))
+                  printf("blk0 k %d s %d j %d row %d act %d bred %.3e ax %.6e yp %.3e -> z %.6e y %.3e lo %.3e hi %.3e\n",
+                         k, s, j, nat_row(j), act[j], bred[j], axp[j], yp[j], z[j], y[j], lo[j], hi[j]);
+#endif
+            update_info();
+#ifdef MPCQ_DEBUG_POLISH
+            if (b < 2 && t == 0) printf("blk %d rd %d admm pri %.3e dua %.3e | polished pri %.3e dua %.3e eps %.3e %.3e\n", (int)b, rd, a_pri, a_dua, pri_res, dua_res, eps_pri, eps_dua);
+#endif
+            if (!have || fmax(pri_res, dua_res) < fmax(b_pri, b_dua)) {
+              have = true;
+              b_pri = pri_res; b_dua = dua_res; b_epri = eps_pri; b_edua = eps_dua;
+              bxf = xf; bxX = xX;
+#pragma unroll
+              for (int j = 0; j < 3; ++j) { bz[j] = z[j]; by[j] = y[j]; }
+            }
+          }
+          const bool good = have && ((b_pri < a_pri && b_dua < a_dua) || (b_pri < a_pri && a_dua < 1e-10) ||
+                                     (b_dua < a_dua && a_pri < 1e-10));
+          if (good) {
+            xf = bxf;
+            xX = bxX;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) { z[j] = bz[j]; y[j] = by[j]; }
+            pol_st = 1;
+            if (status != MPCQ_STATUS_SOLVED && b_pri < b_epri && b_dua < b_edua) status = MPCQ_STATUS_SOLVED;
+          } else {
+            xf = axf;
+            xX = axX;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) { z[j] = az[j]; y[j] = ay[j]; }
+            pol_st = have ? -1 : 0;
+          }
+        }
+      }
     }
     // ------------------------------------------------------------ outputs
     const bool nan_out = status == MPCQ_STATUS_NONFINITE || status == MPCQ_STATUS_FACTOR_FAILED ||
@@ -1522,11 +1719,11 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       if (a.rho_out) a.rho_out[b] = rho_s;
       if (a.info) {
         a.info[4 * b + 0] = n_upd;
-        a.info[4 * b + 1] = 0;
+        a.info[4 * b + 1] = pol_st;
 #ifdef MPCQ_FACTIME
         a.info[4 * b + 2] = (int)(fac_cycles >> 8);  // factorisation cycles / 256 (timing build)
 #else
-        a.info[4 * b + 2] = 0;
+        a.info[4 * b + 2] = pol_rounds;
 #endif
         a.info[4 * b + 3] = 0;
       }
@@ -1538,9 +1735,14 @@ template <int N>
 hipError_t launch_t(bool fused, bool solve, const mpcq_params& p, const LaunchArgs& a,
                     hipStream_t s) {
   const dim3 grid((unsigned)a.batch), block(16 * N);
-  if (!solve) hipLaunchKernelGGL((engine_kernel<N, true, false>), grid, block, 0, s, p, a);
-  else if (fused) hipLaunchKernelGGL((engine_kernel<N, true, true>), grid, block, 0, s, p, a);
-  else hipLaunchKernelGGL((engine_kernel<N, false, true>), grid, block, 0, s, p, a);
+  // polish lives in its own instantiation: the production kernel's code (and its
+  // register allocation in the ADMM loop) does not carry it
+  const bool pol = p.polish != 0;
+  if (!solve) hipLaunchKernelGGL((engine_kernel<N, true, false, false>), grid, block, 0, s, p, a);
+  else if (fused && pol) hipLaunchKernelGGL((engine_kernel<N, true, true, true>), grid, block, 0, s, p, a);
+  else if (fused) hipLaunchKernelGGL((engine_kernel<N, true, true, false>), grid, block, 0, s, p, a);
+  else if (pol) hipLaunchKernelGGL((engine_kernel<N, false, true, true>), grid, block, 0, s, p, a);
+  else hipLaunchKernelGGL((engine_kernel<N, false, true, false>), grid, block, 0, s, p, a);
   return hipGetLastError();
 }
 

@@ -624,6 +624,9 @@ static int polish(Work* W, const mpcq_params* p, Info* admm_info, double* x, dou
       if (rd == 0) { /* OSQP's guess (polish.c form_Ared) */
         if (zs[r] - W->lo[r] < -ys[r]) a = -1;
         else if (W->hi[r] - zs[r] < ys[r]) a = 1;
+        /* equality rows stay in the set even when y is exactly 0 (the GPU
+           factorisation divides by their rho) */
+        if (a == 0 && W->hi[r] - W->lo[r] < RHO_TOL) a = 1;
       } else {       /* keep correctly signed active rows, add violated rows */
         const double tol = 1e-12;
         int eq = W->hi[r] - W->lo[r] < RHO_TOL;

@@ -92,6 +92,7 @@ def test_errors_are_codes_not_crashes(mpcq):
     # bad parameters are rejected before any device work
     bad = mpcq.default_params(alpha=2.5)
     assert lib.mpcq_create(0, 16, C.byref(bad), C.byref(h)) != 0
-    pol = mpcq.default_params(polish=1)  # not in the HIP engine yet: refused, never silently ignored
-    assert lib.mpcq_create(0, 16, C.byref(pol), C.byref(h)) == -4
+    for bad_pol in (dict(polish=3), dict(polish=1, delta=0.0), dict(polish=2, polish_rounds=0)):
+        pol = mpcq.default_params(**bad_pol)
+        assert lib.mpcq_create(0, 16, C.byref(pol), C.byref(h)) == -1, bad_pol
     lib.mpcq_destroy(None)  # destroying NULL returns a code, never crashes

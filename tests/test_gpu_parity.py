@@ -105,3 +105,57 @@ def test_nonfinite_input(eng16, golden16, mpcq):
     assert r["status"][0] == mpcq.STATUS_SOLVED
     assert r["status"][1] == mpcq.STATUS_NONFINITE
     assert np.isnan(r["x"][1]).all()
+
+
+@pytest.mark.parametrize("N", [16, 32])
+def test_polish_reaches_optimum(N, golden16, golden32, oracle, mpcq):
+    """Accurate mode (polish=2, 8 active-set rounds): the GPU's forces land on the
+    exact optimum x* of the reference's QP (certified by its KKT residuals in
+    gen_golden.py) -- independently of the ADMM path -- as the oracle's polish
+    does.  The GPU solves each active-set QP by the method of multipliers on its
+    own factorisation; tolerance POLISH_TOL on the forces."""
+    POLISH_TOL = 1e-8
+    g = golden16 if N == 16 else golden32
+    over = dict(polish=2, polish_rounds=8, polish_refine_iter=10)
+    with mpcq.Engine(N, **over) as e:
+        r = e.qp_solve(g["Ax"], g["l"], g["u"])
+    p = oracle.default_params(**over)
+    B = g["Ax"].shape[0]
+    d_star, d_ora = [], []
+    for b in range(B):
+        o = oracle.qp_solve(N, g["Ax"][b], g["l"][b], g["u"][b], params=p)
+        assert r["status"][b] == o["status"] == 1, (b, r["status"][b], o["status"])
+        assert r["polish"][b] == 1, (b, r["polish"][b], o["polish"])
+        d_star.append(np.abs(r["x"][b][12 * N:] - g["x_star"][b][12 * N:]).max())
+        d_ora.append(np.abs(r["x"][b] - o["x"]).max())
+    print(f"N={N} polish: max|f - f*| {max(d_star):.2e} (median {np.median(d_star):.2e}), "
+          f"max|x - x_oracle| {max(d_ora):.2e}")
+    assert max(d_star) < POLISH_TOL
+    assert max(d_ora) < POLISH_TOL
+
+
+def test_polish_osqp_default_mode(golden16, oracle, mpcq):
+    """polish=1 (OSQP's single active-set guess after SOLVED).  The GPU solves the
+    guessed equality QP to convergence (refinement against the true residuals);
+    OSQP's 3 delta-regularised refinements -- restated by the oracle -- stop
+    ~1e-4 short on these QPs and are sometimes rejected.  So: the GPU accepts
+    wherever the oracle does, and its accepted points sit on x*."""
+    g = golden16
+    with mpcq.Engine(16, polish=1) as e:
+        r = e.qp_solve(g["Ax"], g["l"], g["u"])
+    p = oracle.default_params(polish=1)
+    B = g["Ax"].shape[0]
+    acc_gpu = acc_ora = 0
+    worst = 0.0
+    for b in range(B):
+        o = oracle.qp_solve(16, g["Ax"][b], g["l"][b], g["u"][b], params=p)
+        assert r["status"][b] == o["status"]
+        if o["polish"] == 1:
+            assert r["polish"][b] == 1, b
+        acc_ora += o["polish"] == 1
+        if r["polish"][b] == 1:
+            acc_gpu += 1
+            worst = max(worst, np.abs(r["x"][b][192:] - g["x_star"][b][192:]).max())
+    print(f"polish=1: accepted on {acc_gpu}/{B} (oracle {acc_ora}/{B}), accepted max|f - f*| {worst:.2e}")
+    assert acc_gpu >= acc_ora
+    assert worst < 1e-8

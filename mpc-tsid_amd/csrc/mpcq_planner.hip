@@ -24,14 +24,27 @@ namespace mpcq {
 namespace {
 
 struct PlanShared {
-  double gait[100];
-  double fs[260];
+  alignas(16) double gait[100];
+  alignas(16) double fs[260];
   double v6[33], v7[33];
+  // per phase i of compute_footsteps: cos / sin of the yaw at the phase start and
+  // the displacement dx, dy (FootstepPlanner.py:329-343), one lane per phase
+  double ph_c[20], ph_s[20], ph_dx[20], ph_dy[20];
   // the instance's small inputs: state 0..11, v_ref 12..17, v_cur 18..23,
   // l_feet 24..35, h 36, h_rot 37
   double in[38];
   int flag, reduced, bad;
 };
+
+// LDS -> HBM in 16-B pieces per lane (n even, both sides 16-B aligned)
+__device__ __forceinline__ void copy_out16(double* dst, const double* src, int n, int lane) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    for (int e = lane; e < n / 2; e += 64) reinterpret_cast<d2*>(dst)[e] = reinterpret_cast<const d2*>(src)[e];
+  } else {  // a caller's buffer that is only 8-B aligned
+    for (int e = lane; e < n; e += 64) dst[e] = src[e];
+  }
+}
 
 // numpy.linspace(a, b, n)[i] with endpoint: i * ((b - a) / (n - 1)) + a, last = b
 __device__ __forceinline__ double linspace_at(double a, double b, int n, int i) {
@@ -123,7 +136,7 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
     return;  // the instance's buffers stay as they were (the reference raised)
   }
   if (a.ops & MPCQ_PLAN_ROLL)
-    for (int e = lane; e < 100; e += 64) gg[e] = sh.gait[e];
+    copy_out16(gg, sh.gait, 100, lane);
 
   // ---- compute_footsteps (FootstepPlanner.py:284-361)
   if (a.ops & MPCQ_PLAN_FOOTSTEPS) {
@@ -131,6 +144,27 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
     const double h = sh.in[36];
     const int reduced = sh.reduced;
     for (int e = lane; e < 260; e += 64) sh.fs[e] = (e % 13 == 0) ? sh.gait[5 * (e / 13)] : NAN;
+    // the trigonometry of every phase in parallel (lane i = phase i), so the column
+    // walk below carries no cos / sin on its sequential path; dt_cum is summed in
+    // the reference's order (FootstepPlanner.py:310)
+    if (lane >= 1 && lane < 20) {
+      double dt_cum = 0.0;
+      for (int i = 1; i <= lane; ++i) dt_cum += sh.gait[5 * (i - 1)] * pp.dt;
+      const double angle = vr[5] * dt_cum;
+      const double co = cos(angle), si = sin(angle);
+      double dx, dy;
+      if (vr[5] != 0.0) {
+        dx = (vc[0] * si + vc[1] * (co - 1.0)) / vr[5];
+        dy = (vc[1] * si - vc[0] * (co - 1.0)) / vr[5];
+      } else {
+        dx = vc[0] * dt_cum;
+        dy = vc[1] * dt_cum;
+      }
+      sh.ph_c[lane] = co;
+      sh.ph_s[lane] = si;
+      sh.ph_dx[lane] = dx;
+      sh.ph_dy[lane] = dy;
+    }
     __syncthreads();
     if (lane < 12) {
       const int c = lane, q = c / 3, r = c % 3;
@@ -159,26 +193,15 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
       double prev = l0;  // fsteps[i-1, 1+c]
       sh.fs[1 + c] = l0;
       bool prev_st = sh.gait[1 + q] == 1.0;
-      double dt_cum = 0.0;
       for (int i = 1; i < 20; ++i) {
         const double d = sh.gait[5 * i];
         if (!(d != 0.0)) break;
-        dt_cum += sh.gait[5 * (i - 1)] * pp.dt;
         const bool cur_st = sh.gait[5 * i + 1 + q] == 1.0;
         double v = NAN;
         if (prev_st && cur_st) {
           v = prev;
         } else if (!prev_st && cur_st) {
-          const double angle = vr[5] * dt_cum;
-          const double co = cos(angle), si = sin(angle);
-          double dx, dy;
-          if (vr[5] != 0.0) {
-            dx = (vc[0] * si + vc[1] * (co - 1.0)) / vr[5];
-            dy = (vc[1] * si - vc[0] * (co - 1.0)) / vr[5];
-          } else {
-            dx = vc[0] * dt_cum;
-            dy = vc[1] * dt_cum;
-          }
+          const double co = sh.ph_c[i], si = sh.ph_s[i], dx = sh.ph_dx[i], dy = sh.ph_dy[i];
           // (R @ next_footstep)[r, q] + d[r]; R = [[c, -s, 0], [s, c, 0], [0, 0, 1]]
           const double R0 = r == 0 ? co : (r == 1 ? si : 0.0);
           const double R1 = r == 0 ? -si : (r == 1 ? co : 0.0);
@@ -195,7 +218,7 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
     }
     __syncthreads();
     double* gf = a.fsteps + b * 260;
-    for (int e = lane; e < 260; e += 64) gf[e] = sh.fs[e];
+    copy_out16(gf, sh.fs, 260, lane);
   }
 
   // ---- getRefStates (FootstepPlanner.py:76-159)

@@ -12,6 +12,7 @@ instances (no data-path collective): value = instances solved by all ranks /
 max-over-ranks wall time of the K timed steps.
 
 Workloads (BASELINE.json configs):
+  c1            1 instance per GPU, N=16, static trot    -> latency of one tick
   c2 (default)  1024 instances per GPU, N=16, trot      -> weak scaling
   c3            1024 instances per GPU, N=32, trot      -> weak scaling
   c4            65536 instances in total, N=16, trot    -> strong scaling
@@ -37,6 +38,8 @@ PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 (vector and matrix peaks coincide on gfx950)
 
 CONFIGS = {
+    "c1": dict(total=None, per_gpu=1, N=16, gaits=("trot",), static=True,
+               desc="C1: a single QP, N=16, trot, static xref (latency of one tick)"),
     "c2": dict(total=None, per_gpu=1024, N=16, gaits=("trot",), desc="C2: batch 1024 synthetic instances per GPU, N=16, trot"),
     "c3": dict(total=None, per_gpu=1024, N=32, gaits=("trot",), desc="C3: batch 1024 synthetic instances per GPU, N=32, trot"),
     "c4": dict(total=65536, per_gpu=None, N=16, gaits=("trot",), desc="C4: 65536 synthetic instances sharded over the GPUs, N=16, trot"),
@@ -283,7 +286,11 @@ def main():
     scaling = "weak" if (cfg["per_gpu"] or args.batch > 0) else "strong"
 
     # this rank's contiguous shard of the seeded global synthetic batch (mpcq/shard.py)
-    syn = shard.shard_batch(total, world, rank, N, cfg["gaits"], seed=args.seed)
+    if cfg.get("static"):
+        from mpcq import synth
+        syn = synth.make_batch(total // world, N, gaits=cfg["gaits"], seed=args.seed, static=True)
+    else:
+        syn = shard.shard_batch(total, world, rank, N, cfg["gaits"], seed=args.seed)
     per = int(syn["xref"].shape[0])
     xref_d = torch.from_numpy(np.ascontiguousarray(syn["xref"])).to(dev)
     fs_d = torch.from_numpy(np.ascontiguousarray(syn["fsteps"])).to(dev)
@@ -327,6 +334,15 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
 
     wall_max = shard.max_over_ranks(dist, wall, dev, world)
+
+    # end to end through host buffers (H2D + kernel + D2H, the façade's path):
+    # measured after the timed region, reported beside it, never as `value`
+    e2e = []
+    for _ in range(3):
+        t_ = time.perf_counter()
+        eng.solve(syn["xref"], syn["fsteps"], mpcq.MODE_UPDATE, want_x=False)
+        e2e.append(time.perf_counter() - t_)
+    e2e_ms = float(np.median(e2e)) * 1e3
 
     status = st_d.cpu().numpy()
     iters = it_d.cpu().numpy()
@@ -383,6 +399,8 @@ def main():
             "roofline": roof,
             "roofline_hbm": roof_hbm,
             "kernel_ms_per_launch": avg_ms,
+            "end_to_end_host_ms": e2e_ms,
+            "end_to_end_host_value": per / (e2e_ms * 1e-3),
             "solved_fraction": float(allst[:, 0].sum() / allst[:, 1].sum()),
             "iters": {"median": float(np.median(iters)), "p90": float(np.percentile(iters, 90)),
                       "max": int(iters.max()), "rho_updates_mean": float(info[:, 0].mean())},

@@ -553,6 +553,11 @@ int mpcq_session_create(mpcq_ctx* c, int64_t B, const mpcq_planner_params* pp, c
     delete s;
     return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) for the session failed", tot);
   }
+  if (hipMemset(s->mem, 0, tot) != hipSuccess) {  // every array defined before the first tick
+    (void)hipFree(s->mem);
+    delete s;
+    return fail(MPCQ_E_DEVICE, "hipMemset of the session failed");
+  }
   char* base = (char*)s->mem;
   for (int w = 0; w < MPCQ_SV_COUNT; ++w) s->arr[w] = base + off[w];
   s->warm_x = (double*)(base + o_wx);
@@ -625,9 +630,6 @@ int mpcq_session_create(mpcq_ctx* c, int64_t B, const mpcq_planner_params* pp, c
   put(MPCQ_SV_FSTEPS, h);
   free(h);
   free(hi);
-  if (!err && hipMemset(s->arr[MPCQ_SV_X], 0, s->bytes[MPCQ_SV_X]) != hipSuccess) err = 1;
-  if (!err && hipMemset(s->arr[MPCQ_SV_Y], 0, s->bytes[MPCQ_SV_Y]) != hipSuccess) err = 1;
-  if (!err && hipMemset(s->warm_x, 0, (size_t)B * 24 * N * 8) != hipSuccess) err = 1;
   if (err) { mpcq_session_destroy(s); return fail(MPCQ_E_DEVICE, "initialising the session failed"); }
   *out = s;
   return MPCQ_OK;

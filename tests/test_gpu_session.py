@@ -143,3 +143,26 @@ def test_session_bad_gait_reported(mpcq):
         st = sess.read(mpcq.SV_STATUS)
         assert st[2] == mpcq.STATUS_BAD_GAIT
         assert (np.delete(st, 2) == 1).all()
+
+
+def test_session_api_edges(mpcq):
+    """Arrays are defined before the first tick; bad indices and arguments are
+    API errors, never crashes; an empty planner batch is a no-op."""
+    with mpcq.Engine(16) as eng:
+        with mpcq.Session(eng, 1) as sess:
+            assert not sess.read(mpcq.SV_F0).any()
+            assert sess.read(mpcq.SV_GAIT)[0, :4, 0].tolist() == [1.0, 7.0, 1.0, 7.0]  # walking trot
+            qw = sess.read(mpcq.SV_Q_W)
+            assert qw[0].tolist() == [0.0, 0.0, 0.2027682, 0.0, 0.0, 0.0]  # MPC.py:53-56
+            import ctypes as C
+            from mpcq import _lib as L
+            buf = np.zeros(16)
+            assert L.lib().mpcq_session_read(sess._h, 99, C.c_void_p(buf.ctypes.data), 0) == L.E_INVALID
+            with pytest.raises(mpcq.MpcqError):
+                L.check(L.lib().mpcq_session_tick(sess._h, 0, None, None, None, None, 0))  # v_ref required
+            f0 = sess.tick(np.zeros(6))
+            assert f0.shape == (1, 12) and np.isfinite(f0).all()
+        z = np.zeros((0, 12))
+        st = eng.plan(mpcq.PLAN_TICK, 0, z, np.zeros((0, 3, 4)), np.zeros((0, 6)), np.zeros((0, 20, 5)),
+                      np.zeros(0, np.int32), np.zeros(0), np.zeros((0, 12, 17)), np.zeros((0, 20, 13)))
+        assert st.shape == (0,)

@@ -1295,6 +1295,10 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           for (int rep_ = 0; rep_ < MPCQ_REP_SWEEP; ++rep_) {  // > 1: timing experiments only
           double xp = 0.0;
           if (t < 64) {
+            // the sweeps are every wave's critical path (the other waves of the
+            // instance wait at the barrier): issue them ahead of a co-resident
+            // instance's stage-parallel phases
+            __builtin_amdgcn_s_setprio(3);
             const int gs = cr == 0 ? GS : -GS, bs = cr == 0 ? 12 : -12;
             // rows of step 1: G / H (half 0); S^{-1} of stage kk(-1), never stored (half 1)
             lds_cd* Mp = half == 0 ? GHr + (GS * (cr == 0 ? 1 : N - 1) + RS * rr_)
@@ -1397,6 +1401,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               *(act && half == 0 && s < 12 ? Xp : (lds_d*)&sh.dump[t]) = acc;
               Xp += ws;
             }
+            __builtin_amdgcn_s_setprio(0);
           }
           wave_sync();
           }  // MPCQ_REP_SWEEP

@@ -1271,8 +1271,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             *(cl ? Wna : Wdump) = na;
             *(cl ? Wnb : Wdump) = nb;
           }
-          sync_all();
-          STAMP(3);
+          // (the barrier that publishes bo / na / nb opens ph_sweep)
       };
       auto ph_sweep = [&]() __attribute__((always_inline)) {
           // P5-P7: the state solve on wave 0 alone (no block barrier inside).
@@ -1294,15 +1293,29 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma nounroll
           for (int rep_ = 0; rep_ < MPCQ_REP_SWEEP; ++rep_) {  // > 1: timing experiments only
           double xp = 0.0;
+          // rows of step 1: G / H (half 0); S^{-1} of stage kk(-1), never stored (half 1).
+          // Iteration-invariant: wave 0 reads them before the barrier that publishes
+          // the right-hand sides, so their latency hides behind it.
+          lds_cd* Mp = half == 0 ? GHr + (GS * (cr == 0 ? 1 : N - 1) + RS * rr_)
+                                 : SmR + (GS * (cr == 0 ? -1 : N) + RS * rr_);
+          double g[12];
+          auto row12 = [&](lds_cd* q) __attribute__((always_inline)) {  // 16-B aligned row: 6 ds_read_b128
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+              const dbl2 v = ((lds_cd2*)q)[i];
+              g[2 * i] = v.x;
+              g[2 * i + 1] = v.y;
+            }
+          };
+          if (t < 64) row12(Mp);
+          sync_all();
+          STAMP(3);
           if (t < 64) {
             // the sweeps are every wave's critical path (the other waves of the
             // instance wait at the barrier): issue them ahead of a co-resident
             // instance's stage-parallel phases
             __builtin_amdgcn_s_setprio(3);
             const int gs = cr == 0 ? GS : -GS, bs = cr == 0 ? 12 : -12;
-            // rows of step 1: G / H (half 0); S^{-1} of stage kk(-1), never stored (half 1)
-            lds_cd* Mp = half == 0 ? GHr + (GS * (cr == 0 ? 1 : N - 1) + RS * rr_)
-                                   : SmR + (GS * (cr == 0 ? -1 : N) + RS * rr_);
             lds_cd* BpN = (lds_cd*)&sh.u.it.bo[cr == 0 ? 0 : N - 1][rr_];  // bo; na, nb at +12N, +24N
             lds_d* Yp = (lds_d*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? -1 : N) + rr_);  // w of kk(j-2)
             double src = half == 0 ? bt_at(BpN) : 0.0;  // y_kk(0) (half 0)
@@ -1313,16 +1326,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             const double m0 = half == 0 ? 1.0 : 0.0;
             double bcn = bt_at(BpN) * m0;
             BpN += bs;
-            double g[12], b0 = BpN[0], b1 = BpN[12 * N], b2 = BpN[24 * N];
-            auto row12 = [&](lds_cd* q) __attribute__((always_inline)) {  // 16-B aligned row: 6 ds_read_b128
-#pragma unroll
-              for (int i = 0; i < 6; ++i) {
-                const dbl2 v = ((lds_cd2*)q)[i];
-                g[2 * i] = v.x;
-                g[2 * i + 1] = v.y;
-              }
-            };
-            row12(Mp);
+            double b0 = BpN[0], b1 = BpN[12 * N], b2 = BpN[24 * N];
             Mp += gs;
             BpN += bs;
 #pragma unroll
@@ -1405,22 +1409,24 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           }
           wave_sync();
           }  // MPCQ_REP_SWEEP
-          sync_all();
-          STAMP(7);
       };
       auto ph_recover = [&](double uf, double beta, double& sf, double& sX, double (&ax)[3])
           __attribute__((always_inline)) {
           // P8: forces f_k = F_k (b_f - R B' g) = u - (F W) g, with g = Xd X_{k+1} + Hd X_k
           // on the velocity rows (the states' part of those rows)
           double gv;
-          // all LDS operands of P8 / P9 first (one round trip)
-          const double xa = XSr[oXSp], xb = XSr[oXSp6];
-          sX = XSr[oXS];
+          // the iteration-invariant LDS operands of P8 / P9 are read before the
+          // barrier that ends the sweeps (their latency hides behind it), the
+          // sweep's states after it
           double fwl[6], qll[6];
 #pragma unroll
           for (int i = 0; i < 6; ++i) { fwl[i] = FWr[oFW + i]; qll[i] = QLr[oQLm + i]; }
           const double eXd = Ab[oXd], eHd = Ab[oHdm], eH6 = Ab[oH6m];
           const double cFb = Ab[oFb], cFa = Ab[oFa], cF4 = Ab[oF4], cSw = Ab[oF + 4];
+          sync_all();
+          STAMP(7);
+          const double xa = XSr[oXSp], xb = XSr[oXSp6];
+          sX = XSr[oXS];
           asm volatile("" : : : "memory");
           {
             gv = eXd * sX + eHd * xa;  // used from the lanes of rows 6..11 only

@@ -1328,6 +1328,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             BpN += bs;
             double b0 = BpN[0], b1 = BpN[12 * N], b2 = BpN[24 * N];
             Mp += gs;
+            // first outward step: G_{MID}' (top) / H_{MID+1}' (bottom) columns
+            lds_cd* const MpO = GHr + (GS * (cr == 0 ? MID : MID + 1) + rr_);
             BpN += bs;
 #pragma unroll
             for (int j = 1; j <= MID + 1; ++j) {
@@ -1343,6 +1345,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
                 row12(half == 0 ? GHr + RS * rr_ : Mp);
                 lds_cd* qb = (lds_cd*)&sh.u.it.bo[MID][rr_];
                 b0 = qb[0]; b1 = qb[12 * N]; b2 = qb[24 * N];
+              } else {  // the last step: the first outward step's columns
+#pragma unroll
+                for (int i = 0; i < 12; ++i) g[i] = MpO[RS * i];
               }
               asm volatile("" : : : "memory");  // the prefetch is issued here, not sunk to its use
               double s_in = src;
@@ -1375,11 +1380,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             // repeats half 0).  The bottom row's last step (kk = N) is idle: its loads stay
             // inside the shared memory block and its store goes to the lane's sink.
             const int ms = cr == 0 ? -GS : GS, ws = cr == 0 ? -12 : 12;
-            lds_cd* MpN = GHr + (GS * (cr == 0 ? MID : MID + 1) + rr_);
+            lds_cd* MpN = MpO;  // its first columns were read during the meeting step
             lds_cd* WpN = (lds_cd*)&sh.u.it.yv[cr == 0 ? MID - 1 : MID + 1][rr_];
             lds_d* Xp = (lds_d*)&sh.u.it.xs[cr == 0 ? MID : MID + 2][rr_];
-#pragma unroll
-            for (int i = 0; i < 12; ++i) g[i] = MpN[RS * i];
             MpN += ms;
             wave_sync();  // the w written by half 1
             double bq = WpN[0];

@@ -259,17 +259,24 @@ __device__ __forceinline__ void gj_step(double (&R)[12], int me, bool& ok) {
   if (!(d > 0.0) && me == PV) printf("pivot fail blk %d thr %d PV %d d %g\n", (int)blockIdx.x, (int)threadIdx.x, PV, d);
 #endif
   if (!(d > 0.0)) ok = false;
-  const double id = 1.0 / d;
-  const double mrp = R[PV];
+  // 1/d: v_rcp_f64 and two Newton steps (the pivots are positive and far from the
+  // denormal / overflow range, so the IEEE division's scaling and fix-up are not needed)
+  double id = __builtin_amdgcn_rcp(d);
+  double e_ = fma(-d, id, 1.0);
+  id = fma(id, e_, id);
+  e_ = fma(-d, id, 1.0);
+  id = fma(id, e_, id);
+  // one multiplier per row: the pivot row becomes p / d, every other row
+  // R - (R[PV] / d) p, so each entry is a single FMA on the broadcast pivot row
   const bool isp = me == PV;
+  const double a = isp ? id : -(R[PV] * id);
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
-    const double pj = (j == PV) ? d : rbc<LN(PV)>(R[j]);
-    double v;
-    if (isp) v = (j == PV) ? id : pj * id;
-    else v = (j == PV) ? -mrp * id : R[j] - mrp * pj * id;
-    R[j] = v;
+    if (j == PV) continue;
+    const double base = isp ? 0.0 : R[j];
+    R[j] = fma(a, rbc<LN(PV)>(R[j]), base);
   }
+  R[PV] = a;
 }
 template <int... P>
 __device__ __forceinline__ void gj_seq(double (&R)[12], int me, bool& ok, std::integer_sequence<int, P...>) {

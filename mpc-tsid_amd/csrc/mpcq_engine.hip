@@ -852,10 +852,18 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       // (St), giving G_k -> GH[k]; lower C = L_{k+1}' (row ph) against U_{k+1}^{-1}
       // (Sb), giving H_k -> GH[k+1].  Ro -= (C S^{-1}) C'.  Products run block by
       // block (a compiler fence per block keeps the loads from piling up).
+      // Every row's D / L coefficients depend only on its own stage and the next
+      // one, all final here: each lane builds its rows before the serial steps
+      // (in parallel, one LDS round trip) instead of inside them.
+      double Dr0[12], cta, ct6[6], cba, cb6[6];
+      Drow(k, ph, dgX, Dr0);
+      Ctop(k, ph, cta, ct6);                      // used from k >= 1 only
+      Cbot(k < N - 1 ? k + 1 : k, ph, cba, cb6);  // used from k < N-1 only
       auto couple = [&](bool upper, double (&Ro)[12]) __attribute__((always_inline)) {
-        double ca, c6[6];
-        if (upper) Ctop(k, ph, ca, c6);
-        else Cbot(k + 1, ph, ca, c6);
+        const double ca = upper ? cta : cba;
+        double c6[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) c6[j] = upper ? ct6[j] : cb6[j];
         double* const Cb = upper ? Lt : Lb;  // compact rows: 7 per row
         const double* const Sp = upper ? St : Sb;
         if (cl) {
@@ -903,7 +911,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         if (top || bot || mrow) {
           const bool useT = (top && k > 0) || mrow, useB = (bot && k < N - 1) || mrow;
           double Ro[12];
-          Drow(k, ph, dgX, Ro);  // reads GH[k], GH[k+1] (Q, rho) before any G / H lands there
+#pragma unroll
+          for (int ci = 0; ci < 12; ++ci) Ro[ci] = Dr0[ci];
           if (useT) couple(true, Ro);
           if (useB) couple(false, Ro);
           gj12(Ro, ph, ok);

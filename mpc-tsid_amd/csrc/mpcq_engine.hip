@@ -1369,6 +1369,10 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               double s_in = src;
               if (j == MID + 1) s_in = half == 0 ? row_pair_sum(src) - ((b0 + b1) + b2) : src;
               const double acc = bdot12(gc, s_in, bc);
+              // the next right-hand side is summed after the chain: its loads were
+              // issued at the end of the previous step, and summing them ahead of the
+              // chain would put their LDS latency on the critical path
+              asm volatile("" : "+v"(b0), "+v"(b1), "+v"(b2));
               if (j < MID) bcn = ((b0 + b1) + b2) * m0;
               if (j + 2 <= MID) {
                 b0 = BpN[0]; b1 = BpN[12 * N]; b2 = BpN[24 * N];

@@ -1300,9 +1300,6 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           // solves x_m = M^{-1} (y_m + v_m - b_m) (top and bottom rows joined by
           // permlane16_swap), half 1 the last top w.  Then the outward sweeps.
           const int half = (t >> 5) & 1;
-          auto bt_at = [&](lds_cd* q) __attribute__((always_inline)) {
-            return (q[0] + q[12 * N]) + q[24 * N];
-          };
 #ifndef MPCQ_REP_SWEEP
 #define MPCQ_REP_SWEEP 1
 #endif
@@ -1334,14 +1331,18 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             const int gs = cr == 0 ? GS : -GS, bs = cr == 0 ? 12 : -12;
             lds_cd* BpN = (lds_cd*)&sh.u.it.bo[cr == 0 ? 0 : N - 1][rr_];  // bo; na, nb at +12N, +24N
             lds_d* Yp = (lds_d*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? -1 : N) + rr_);  // w of kk(j-2)
-            double src = half == 0 ? bt_at(BpN) : 0.0;  // y_kk(0) (half 0)
-            BpN += bs;
             // right-hand sides run two steps ahead: step j sums the one of step j+1
             // (loaded during step j-1) and loads the one of step j+2; half 1 (the w
-            // products) starts its chain from 0
+            // products) starts its chain from 0.  The first two (y_kk(0) and step 1's)
+            // are loaded together and waited for once: they were published by the
+            // barrier just passed, so this round trip is on the critical path.
             const double m0 = half == 0 ? 1.0 : 0.0;
-            double bcn = bt_at(BpN) * m0;
-            BpN += bs;
+            double s0 = BpN[0], s1 = BpN[12 * N], s2 = BpN[24 * N];
+            double c0 = BpN[bs], c1 = BpN[bs + 12 * N], c2 = BpN[bs + 24 * N];
+            asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(c0), "+v"(c1), "+v"(c2));
+            double src = half == 0 ? (s0 + s1) + s2 : 0.0;  // y_kk(0) (half 0)
+            double bcn = ((c0 + c1) + c2) * m0;
+            BpN += 2 * bs;
             double b0 = BpN[0], b1 = BpN[12 * N], b2 = BpN[24 * N];
             Mp += gs;
             // first outward step: G_{MID}' (top) / H_{MID+1}' (bottom) columns

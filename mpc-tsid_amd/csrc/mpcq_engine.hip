@@ -873,14 +873,20 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         }
         wave_sync();  // C rows visible (and this row's reads of GH[k], GH[k+1] are done)
         const int ar = ph < 6 ? ph : ph - 6;
+        // column by column: the seven operands of one column are loaded together
+        // and waited for once (row blocks waited load by load under the register
+        // pressure here)
         double G[12];
 #pragma unroll
-        for (int ci = 0; ci < 12; ++ci) G[ci] = ca * Sp[12 * ar + ci];
-        asm volatile("" ::: "memory");
+        for (int ci = 0; ci < 12; ++ci) {
+          double sv[7];
+          sv[0] = Sp[12 * ar + ci];
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
+          for (int j = 0; j < 6; ++j) sv[1 + j] = Sp[12 * (6 + j) + ci];
+          double gv = ca * sv[0];
 #pragma unroll
-          for (int ci = 0; ci < 12; ++ci) G[ci] = fma(c6[j], Sp[12 * (6 + j) + ci], G[ci]);
+          for (int j = 0; j < 6; ++j) gv = fma(c6[j], sv[1 + j], gv);
+          G[ci] = gv;
           asm volatile("" ::: "memory");
         }
         if (cl) {

@@ -286,6 +286,27 @@ __device__ __forceinline__ void gj12(double (&R)[12], int me, bool& ok) {
   gj_seq(R, me, ok, std::make_integer_sequence<int, 12>{});
 }
 
+// Ro -= G C' for one 12x12 coupling block C held one row per column lane in
+// compact form (ca on column CI mod 6, c6 on the velocity columns): column CI of
+// the product takes row CI of C from lane LN(CI) by row broadcast
+template <int CI>
+__device__ __forceinline__ void schur_col(double (&Ro)[12], const double (&G)[12], double ca,
+                                          const double (&c6)[6]) {
+  constexpr int J = LN(CI);
+  double a0 = G[CI < 6 ? CI : CI - 6] * rbc<J>(ca), a1 = G[6] * rbc<J>(c6[0]);
+  a0 = fma(G[7], rbc<J>(c6[1]), a0);
+  a1 = fma(G[8], rbc<J>(c6[2]), a1);
+  a0 = fma(G[9], rbc<J>(c6[3]), a0);
+  a1 = fma(G[10], rbc<J>(c6[4]), a1);
+  a0 = fma(G[11], rbc<J>(c6[5]), a0);
+  Ro[CI] -= a0 + a1;
+}
+template <int... C>
+__device__ __forceinline__ void schur_cols(double (&Ro)[12], const double (&G)[12], double ca,
+                                           const double (&c6)[6], std::integer_sequence<int, C...>) {
+  (schur_col<C>(Ro, G, ca, c6), ...);
+}
+
 // ---------------------------------------------------------------------------
 // Formulation pieces (restating MPC.py; oracle/mpcq_oracle.c is the CPU twin)
 
@@ -389,7 +410,7 @@ struct Smem {
       double xs[N + 1][12];  // X_k (xs[k+1] = X_{k+1}, stage k's states)
     } it;
     struct {
-      double St[144], Sb[144], Lt[144], Lb[144];  // sweep hand-offs of the factorisation
+      double St[144], Sb[144];  // sweep hand-offs of the factorisation
     } fa;
   } u;
   double red[12 * N];  // per-row partial reductions
@@ -843,8 +864,6 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       // L goes to LDS entry by entry, G / H straight to their GH slot.
       double* const St = sh.u.fa.St;
       double* const Sb = sh.u.fa.Sb;
-      double* const Lt = sh.u.fa.Lt;
-      double* const Lb = sh.u.fa.Lb;
       // Step j < MID: top row k = j (C = L_k against S_{k-1}^{-1}) and bottom row
       // k = N-1-j > MID (C = L_{k+1}' against U_{k+1}^{-1}) in parallel; step MID:
       // the meeting row (both couplings).  G_k -> GH[k], H_k -> GH[k+1], M^{-1} -> GH[0].
@@ -864,14 +883,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         double c6[6];
 #pragma unroll
         for (int j = 0; j < 6; ++j) c6[j] = upper ? ct6[j] : cb6[j];
-        double* const Cb = upper ? Lt : Lb;  // compact rows: 7 per row
         const double* const Sp = upper ? St : Sb;
-        if (cl) {
-          Cb[7 * ph] = ca;
-#pragma unroll
-          for (int j = 0; j < 6; ++j) Cb[7 * ph + 1 + j] = c6[j];
-        }
-        wave_sync();  // C rows visible (and this row's reads of GH[k], GH[k+1] are done)
+        wave_sync();  // this row's reads of GH[k], GH[k+1] are done
         const int ar = ph < 6 ? ph : ph - 6;
         // column by column: the seven operands of one column are loaded together
         // and waited for once (row blocks waited load by load under the register
@@ -894,18 +907,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma unroll
           for (int ci = 0; ci < 12; ++ci) Gd[ci] = -G[ci];  // stored negated
         }
-#pragma unroll
-        for (int ci = 0; ci < 12; ++ci) {
-          const double* const cr = Cb + 7 * ci;
-          double a0 = G[ci < 6 ? ci : ci - 6] * cr[0], a1 = G[6] * cr[1];
-          a0 = fma(G[7], cr[2], a0);
-          a1 = fma(G[8], cr[3], a1);
-          a0 = fma(G[9], cr[4], a0);
-          a1 = fma(G[10], cr[5], a1);
-          a0 = fma(G[11], cr[6], a0);
-          Ro[ci] -= a0 + a1;
-          asm volatile("" ::: "memory");
-        }
+        schur_cols(Ro, G, ca, c6, std::make_integer_sequence<int, 12>{});
       };
       // Step j < MID: top row k = j and bottom row k = N-1-j > MID in parallel; step
       // MID: the meeting row (both couplings).  M^{-1} -> GH[0].

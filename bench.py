@@ -55,10 +55,20 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override instances per GPU")
-    ap.add_argument("--polish", action="store_true", help="accurate mode: polish=2, 8 rounds, 10 refinements")
-    ap.add_argument("--cpu-sample", type=int, default=12288,
-                    help="instances in the CPU-baseline sample, cycling over the rank-0 batch (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--polish", dest="polish", action="store_true", default=True,
+                    help="(default) accuracy mode: OSQP polish after the ADMM (polish=2, up to 8 active-set "
+                         "rounds, 10 refinements): forces on the QP's certified optimum")
+    ap.add_argument("--no-polish", dest="polish", action="store_false",
+                    help="the ADMM alone (OSQP 0.6 defaults, polish off as in MPC.py:414-416)")
+    ap.add_argument("--rho-interval", type=int, default=0,
+                    help="override adaptive_rho_interval (0 = the library default)")
+    ap.add_argument("--cpu-sample", type=float, default=1.5,
+                    help="seconds of CPU work per CPU-baseline run (3 warm-up + 10 timed runs, each over "
+                         "instances cycling through the rank-0 batch; 0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
+    ap.add_argument("--certify", type=int, default=1024,
+                    help="instances (the first ones of rank 0) whose forces are checked against the "
+                         "KKT-certified optimum (-1 = all, 0 = skip)")
     ap.add_argument("--gather", action="store_true", help="include an RCCL all-gather of f0 in the timed region")
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--mode", default="qp", choices=("qp", "plan", "tick"),
@@ -68,16 +78,22 @@ def parse():
     return ap.parse_args()
 
 
-def load_traffic(tag: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+def load_pmc(tag: str) -> dict:
+    """Per-launch PMC figures (HBM bytes, issued FP64 flops, that run's kernel ms)
+    from the committed rocprofv3 summary profiles/pmc_traffic.json, if any."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        e = d.get(tag)
-        return float(e["bytes_per_launch"]) if e else None
+        return dict(d.get(tag) or {})
     except (OSError, ValueError):
-        return None
+        return {}
+
+
+def load_traffic(tag: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    v = load_pmc(tag).get("bytes_per_launch")
+    return float(v) if v is not None else None
 
 
 def _dist_setup():
@@ -169,7 +185,7 @@ def main_plan(args):
         if world == 1 and args.cpu_sample > 0:
             from oracle import oracle as O
             O.build()
-            ns = min(args.cpu_sample, per)
+            ns = min(4096, per)
             pls = [O.Planner(N, gaits[b]) for b in range(ns)]
             t = time.perf_counter()
             reps = 0
@@ -224,7 +240,7 @@ def main_tick(args):
                "data": "synthetic robots, virtual robot closed loop (state from the previous prediction)",
                "config": {"workload": f"session tick, {per} robots per GPU, N={N}, gaits {list(cfg['gaits'])}",
                           "horizon": N, "parallelism": f"shard{world}"},
-               "roofline": {"bound": "mfma", "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+               "roofline": {"bound": "valu_fp64", "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                             "frac": ach / PEAK_FP64_TFLOPS, "traffic": None,
                             "note": "engine kernel of the last tick: model.flops(measured iterations, rho updates "
                                     "taken as 0 -- a lower bound) / its HIP-event time"},
@@ -252,6 +268,52 @@ def main_tick(args):
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_cpus():
+    """CPUs this process may use on this host: affinity mask, capped by a cgroup CPU quota."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    return dict(nproc=os.cpu_count(), affinity=aff, cgroup_quota=quota, usable=usable, model=model)
+
+
+def cpu_baseline(O, syn, per, params, threads, seconds):
+    """The oracle's native build (-O3 -march=native, OpenMP over `threads`) on
+    instances cycling through this rank's batch: 3 warm-up runs, then the median
+    of 10 timed runs, each sized to about `seconds` of work."""
+    def run(ns):
+        sel = np.arange(ns) % per
+        xr, fs = syn["xref"][sel], syn["fsteps"][sel]
+        t = time.perf_counter()
+        O.solve_batch(xr, fs, 0, params=params, nthreads=threads, native=True)
+        return time.perf_counter() - t
+
+    O.native_lib()
+    ns = 2 * threads
+    t = run(ns)                                  # warm-up 1 (also sizes the runs)
+    ns = max(threads, int(ns * seconds / max(t, 1e-3)))
+    run(ns)                                      # warm-ups 2 and 3
+    run(ns)
+    times = [run(ns) for _ in range(10)]
+    med = float(np.median(times))
+    return ns / med, ns, times
 
 
 def main():
@@ -300,15 +362,20 @@ def main():
     info_d = torch.empty((per, 4), dtype=torch.int32, device=dev)
 
     over = dict(polish=2, polish_rounds=8, polish_refine_iter=10) if args.polish else {}
+    if args.rho_interval > 0:
+        over["adaptive_rho_interval"] = args.rho_interval
     eng = mpcq.Engine(N, device=local, **over)
     # a dedicated (non-default) HIP stream: the engine launches on it and the
     # HIP events that time the kernel are recorded on the same stream
     stream = torch.cuda.Stream(dev)
     eng.set_stream(stream.cuda_stream)
 
-    def step():
+    def launch(x_ptr=0, y_ptr=0):
         eng.solve_device(per, xref_d.data_ptr(), fs_d.data_ptr(), f0_d.data_ptr(), st_d.data_ptr(),
-                         it_d.data_ptr(), info_ptr=info_d.data_ptr(), asynchronous=True)
+                         it_d.data_ptr(), x_ptr=x_ptr, y_ptr=y_ptr, info_ptr=info_d.data_ptr(), asynchronous=True)
+
+    def step():
+        launch()
         if args.gather and world > 1:
             shard.gather_rows(dist, f0_d, total, world, rank)  # forces of every instance on every rank
 
@@ -319,30 +386,21 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
+    evs[0].record(stream)
+    for i in range(args.steps):
         step()
-    ev1.record(stream)
+        evs[i + 1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
+    launch_ms = np.array([evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]) if args.steps else np.zeros(1)
+    kern_ms = float(launch_ms.mean())
 
     wall_max = shard.max_over_ranks(dist, wall, dev, world)
-
-    # end to end through host buffers (H2D + kernel + D2H, the façade's path):
-    # measured after the timed region, reported beside it, never as `value`
-    e2e = []
-    for _ in range(3):
-        t_ = time.perf_counter()
-        eng.solve(syn["xref"], syn["fsteps"], mpcq.MODE_UPDATE, want_x=False)
-        e2e.append(time.perf_counter() - t_)
-    e2e_ms = float(np.median(e2e)) * 1e3
 
     status = st_d.cpu().numpy()
     iters = it_d.cpu().numpy()
@@ -352,8 +410,29 @@ def main():
     # per-launch algorithmic work of this rank
     p = eng.params
     fl = model.flops(N, iters, info[:, 0], p.check_termination,
-                     p.adaptive_rho_interval if p.adaptive_rho else 0, p.scaling).sum()
+                     p.adaptive_rho_interval if p.adaptive_rho else 0, p.scaling,
+                     polish_rounds=info[:, 2] if args.polish else None,
+                     polish_solves=1 + max(p.polish_refine_iter, 10)).sum()
+    fl_dense = model.flops(N, iters, info[:, 0], p.check_termination,
+                           p.adaptive_rho_interval if p.adaptive_rho else 0, p.scaling,
+                           polish_rounds=info[:, 2] if args.polish else None,
+                           polish_solves=1 + max(p.polish_refine_iter, 10), structured=False).sum()
     by = model.bytes_per_instance(N) * per
+
+    # after the timed region: one more launch that also returns x and y (the
+    # certificate's active-set seed), and the host-buffer end-to-end path
+    x_d = torch.empty((per, 24 * N), dtype=torch.float64, device=dev)
+    y_d = torch.empty((per, 44 * N), dtype=torch.float64, device=dev)
+    launch(x_d.data_ptr(), y_d.data_ptr())
+    torch.cuda.synchronize(dev)
+    same = bool(np.array_equal(f0_d.cpu().numpy(), f0, equal_nan=True))
+    xg, yg = x_d.cpu().numpy(), y_d.cpu().numpy()
+    e2e = []
+    for _ in range(3):
+        t_ = time.perf_counter()
+        eng.solve(syn["xref"], syn["fsteps"], mpcq.MODE_UPDATE, want_x=False)
+        e2e.append(time.perf_counter() - t_)
+    e2e_ms = float(np.median(e2e)) * 1e3
 
     stats = torch.tensor([solved, per, fl, by, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -364,20 +443,31 @@ def main():
         allst = stats.cpu().numpy()[None]
 
     if rank == 0:
-        value = float(allst[:, 1].sum()) * args.steps / wall_max
-        avg_ms = float(kern_ms)
+        # QP instances solved (status 1 solved / 2 solved inaccurate) by all ranks per second
+        value = float(allst[:, 0].sum()) * args.steps / wall_max
         fl0, by0 = float(allst[0, 2]), float(allst[0, 3])
-        tr = load_traffic(f"{args.config}_N{N}_B{per}")
-        roof = {"bound": "mfma", "achieved": fl0 / (avg_ms * 1e-3) / 1e12, "peak": PEAK_FP64_TFLOPS,
-                "unit": "TFLOP/s", "frac": None, "traffic": tr,
-                "note": "fp64: the kernel runs on VALU FMA; gfx950's FP64 MFMA and vector peaks coincide (78.6 TF). "
-                        "achieved = model.flops(measured iterations, rho updates) per launch / mean launch time; "
-                        "traffic = HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/pmc_traffic.json)"}
+        tag = f"{args.config}_N{N}_B{per}" + ("_polish" if args.polish else "")
+        pmc = load_pmc(tag)
+        roof = {"bound": "valu_fp64", "achieved": fl0 / (kern_ms * 1e-3) / 1e12, "peak": PEAK_FP64_TFLOPS,
+                "unit": "TFLOP/s", "frac": None, "traffic": pmc.get("bytes_per_launch"),
+                "achieved_dense_model": fl_dense / (kern_ms * 1e-3) / 1e12,
+                "achieved_counters": (pmc["fp64_flops_per_launch"] / (pmc["kernel_ms"] * 1e-3) / 1e12
+                                      if pmc.get("fp64_flops_per_launch") and pmc.get("kernel_ms") else None),
+                "note": "FP64 on VALU FMA (no MFMA: the stage blocks are 12x12 with sequential recurrences; gfx950's "
+                        "FP64 vector and matrix peaks coincide, 78.6 TF). achieved = mpcq/model.py algorithmic flops "
+                        "(measured iterations, rho updates, polish rounds; structural zeros excluded) per launch / mean "
+                        "HIP-event launch time; achieved_dense_model counts the dense 24x24 stage blocks (round-1 model); "
+                        "achieved_counters = issued FP64 lane-ops from the committed rocprofv3 PMC pass "
+                        "(2 SQ_INSTS_VALU_FMA_F64 + MUL_F64 + ADD_F64) x 64 / that run's kernel time; traffic = HBM "
+                        "bytes per launch from the PMC FETCH_SIZE / WRITE_SIZE passes (profiles/pmc_traffic.json)"}
         roof["frac"] = roof["achieved"] / roof["peak"]
-        hbm_ach = by0 / (avg_ms * 1e-3) / 1e9
+        hbm_ach = by0 / (kern_ms * 1e-3) / 1e9
         roof_hbm = {"bound": "hbm", "achieved": hbm_ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": hbm_ach / PEAK_HBM_GBS, "traffic": tr,
+                    "frac": hbm_ach / PEAK_HBM_GBS, "traffic": pmc.get("bytes_per_launch"),
                     "note": f"algorithmic bytes {model.bytes_per_instance(N)} B/instance x {per} instances per launch"}
+        edges = np.arange(0, p.max_iter + 251, 250)
+        hist, _ = np.histogram(iters, bins=edges)
+        sts, cnt = np.unique(status, return_counts=True)
         out = {
             "metric": METRIC,
             "value": value,
@@ -393,37 +483,69 @@ def main():
             "data": "synthetic (seeded FootstepPlanner-shaped xref/fsteps, mpcq.synth)",
             "config": {"workload": cfg["desc"], "instances_per_gpu": per, "instances_total": total,
                        "horizon": N, "gaits": list(cfg["gaits"]),
-                       "solver": "OSQP-0.6 ADMM restated (eps 1e-7, rho 0.1, sigma 1e-6, alpha 1.6, Ruiz 10, adaptive rho/100)"
-                       + (" + active-set polish" if args.polish else ""),
+                       "solver": (f"OSQP-0.6 ADMM restated (eps 1e-7, rho 0.1, sigma 1e-6, alpha 1.6, Ruiz 10, "
+                                  f"adaptive rho every {p.adaptive_rho_interval})")
+                       + (" + OSQP polish (active-set rounds <= 8, 10 refinements)" if args.polish else ", polish off"),
                        "parallelism": f"shard{world}" + ("+gather" if args.gather else "")},
             "roofline": roof,
             "roofline_hbm": roof_hbm,
-            "kernel_ms_per_launch": avg_ms,
+            "kernel_ms_per_launch": kern_ms,
+            "kernel_ms_launches": {"median": float(np.median(launch_ms)), "min": float(launch_ms.min()),
+                                   "max": float(launch_ms.max())},
             "end_to_end_host_ms": e2e_ms,
             "end_to_end_host_value": per / (e2e_ms * 1e-3),
             "solved_fraction": float(allst[:, 0].sum() / allst[:, 1].sum()),
+            "status_hist": {int(a): int(b) for a, b in zip(sts, cnt)},
             "iters": {"median": float(np.median(iters)), "p90": float(np.percentile(iters, 90)),
-                      "max": int(iters.max()), "rho_updates_mean": float(info[:, 0].mean())},
+                      "max": int(iters.max()), "rho_updates_mean": float(info[:, 0].mean()),
+                      "hist_edges_step": 250, "hist": hist.tolist()},
         }
-        if world == 1 and args.cpu_sample > 0:
+        if args.polish:
+            out["polish"] = {"accepted_fraction": float((info[:, 1] == 1).mean()),
+                             "rounds_mean": float(info[:, 2].mean()), "rounds_max": int(info[:, 2].max())}
+        if world == 1 and (args.cpu_sample > 0 or args.certify != 0):
             from oracle import oracle as O
             O.build()
-            ns = args.cpu_sample
-            sel = np.arange(ns) % per  # cycle over the GPU batch: same instance mix
-            thr = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-            op = O.default_params(**over)
+        par = {"repeat_launch_bitwise_equal": same}
+        if world == 1 and args.certify != 0:
+            from oracle import certify
+            nc = per if args.certify < 0 else min(args.certify, per)
             t = time.perf_counter()
-            ro = O.solve_batch(syn["xref"][sel], syn["fsteps"][sel], 0, params=op, nthreads=thr)
-            tc = time.perf_counter() - t
-            nc = min(ns, per)
-            df = np.abs(ro["f0"][:nc] - f0[:nc]).max(axis=1)
-            out["cpu_baseline"] = {"value": ns / tc, "unit": "QP instances/s", "cores": thr, "kind": "port",
-                                   "sample": f"{ns} instances cycling over the rank-0 batch of {per}, oracle/mpcq_oracle.c "
-                                             f"(C restatement of MPC.py + OSQP 0.6 ADMM), OpenMP over {thr} threads, {tc:.1f} s"}
-            out["parity"] = {"max_abs_df0_vs_osqp_restatement": float(df.max()),
-                             "median_abs_df0_vs_osqp_restatement": float(np.median(df)),
-                             "status_agree": float((ro["status"][:nc] == status[:nc]).mean()),
-                             "iters_agree": float((ro["iters"][:nc] == iters[:nc]).mean())}
+            ix = np.arange(nc)
+            res = [certify.certified_forces(syn["xref"][ix], syn["fsteps"][ix], xg[ix], yg[ix])]
+            fstar = np.concatenate([r[0] for r in res])
+            kkt = np.concatenate([r[1] for r in res])
+            okc = np.concatenate([r[2] for r in res])
+            dfo = np.abs(f0[:nc] - fstar).max(axis=1)
+            par.update({"max_abs_df0_vs_optimum": float(dfo.max()),
+                        "median_abs_df0_vs_optimum": float(np.median(dfo)),
+                        "optimum_certified_fraction": float(okc.mean()), "optimum_kkt_max": float(kkt.max()),
+                        "optimum_instances": int(nc), "optimum_seconds": time.perf_counter() - t,
+                        "optimum": "x* of each instance's QP (oracle formulation, pinned to the reference's A/l/u): "
+                                   "active-set solve of the unscaled KKT seeded by the GPU's (x, y), certified by "
+                                   "KKT residuals < 1e-9 (oracle/certify.py)"})
+        if world == 1 and args.cpu_sample > 0:
+            hc = host_cpus()
+            thr = args.cpu_threads or hc["usable"]
+            op = O.default_params(**over)
+            rate, ns, times = cpu_baseline(O, syn, per, op, thr, args.cpu_sample)
+            out["cpu_baseline"] = {"value": rate, "unit": "QP instances/s", "cores": thr, "kind": "port",
+                                   "host": hc,
+                                   "sample": f"{ns} instances per run cycling over the rank-0 batch of {per}; "
+                                             "oracle/mpcq_oracle.c (C restatement of MPC.py + OSQP 0.6 ADMM"
+                                             + (" + polish" if args.polish else "") + ") built -O3 -march=native "
+                                             f"on this host, OpenMP over {thr} threads; 3 warm-up runs, median of "
+                                             f"10 ({min(times):.2f}-{max(times):.2f} s per run)"}
+            # the checker build (the rounding the tests pin) against the GPU on a sample
+            nck = min(per, 256)
+            ro = O.solve_batch(syn["xref"][:nck], syn["fsteps"][:nck], 0, params=op, nthreads=thr)
+            df = np.abs(ro["f0"] - f0[:nck]).max(axis=1)
+            par.update({"max_abs_df0_vs_osqp_restatement": float(df.max()),
+                        "median_abs_df0_vs_osqp_restatement": float(np.median(df)),
+                        "restatement_instances": nck,
+                        "status_agree": float((ro["status"] == status[:nck]).mean()),
+                        "iters_agree": float((ro["iters"] == iters[:nck]).mean())})
+        out["parity"] = par
         print(json.dumps(out), flush=True)
 
     eng.close()

@@ -6,8 +6,8 @@ status, iterations and the 4-int info record.
 
 Flops (float64, a multiply and an add count as two): what the algorithm
 needs per instance, counted on the structured operators the kernel applies
-(zeros of the dense 24x24 stage blocks are counted; idle lanes are not):
-  F = F_form + F_scale + (1 + R) F_fact + K F_iter + C F_check
+(structural zeros excluded; see flops_components):
+  F = F_form + F_scale + (1 + R) F_fact + K F_iter + C F_check (+ polish)
 with K ADMM iterations, R rho updates (refactorisations) and C residual
 evaluations (every check_termination / adaptive-rho iteration), all three
 measured per instance by the kernel.
@@ -27,32 +27,64 @@ def bytes_per_instance(N: int, with_x: bool = False, with_y: bool = False) -> in
     return b_in + b_out
 
 
-def flops_components(N: int, scaling_iters: int = 10) -> dict:
+def flops_components(N: int, scaling_iters: int = 10, structured: bool = True) -> dict:
+    """Flops per instance of each phase.
+
+    structured=True (the default, what bench.py reports): the useful
+    operations of the engine's algorithm, structural zeros excluded -- the
+    forces eliminated per stage through the 12x12 block K_ff^-1 (Gauss-Jordan,
+    12 x 12 x 11 FMAs), F W and Q = W' F W on the six rows B touches (B's
+    position rows are dt/m on one force column each), the 12x12 state system
+    solved two-ended with 12x12 Schur couplings that are seven columns wide,
+    and per iteration the 12x12 sweep products, the force recovery and the
+    row updates.  Shadow lanes and masked terms the kernel issues are not
+    counted (the PMC pass's issued FP64 lane-ops count them).
+
+    structured=False: the round-1 model, dense 24x24 stage blocks with their
+    zeros counted (an upper bound, kept for comparison)."""
     n, m, nnz = 24 * N, 44 * N, 126 * N - 18
     form = 375 * N                                      # B blocks + bounds
     scale = scaling_iters * (4 * nnz + 2 * (n + m) + 4 * n) + 2 * m
-    # per stage: K_k from the 56 rows touching it (~2.1k), C_k (~0.2k),
-    # C Y (24x12x12), Schur update (24x24x12), Gauss-Jordan inverse (2*24^3),
-    # Gamma = S^-1_{X,:} C (12x12x24)
-    fact = N * (2100 + 200 + 2 * 24 * 12 * 12 + 2 * 24 * 24 * 12 + 2 * 24 ** 3 + 2 * 12 * 12 * 24)
-    # per stage: alpha (12x24), forward step (12x12), C s, bhat, S^-1 bhat (24x24),
-    # C' t, backward step, S^-1_{:,X} v (24x12); then A'w, A x, vector updates
-    it = N * (576 + 288 + 180 + 24 + 1152 + 180 + 288 + 600) + 4 * nnz + 10 * m + 5 * n
     check = 4 * nnz + n + 6 * (n + m)
-    return dict(form=form, scale=scale, fact=fact, iter=it, check=check)
+    if not structured:
+        fact = N * (2100 + 200 + 2 * 24 * 12 * 12 + 2 * 24 * 24 * 12 + 2 * 24 ** 3 + 2 * 12 * 12 * 24)
+        it = N * (576 + 288 + 180 + 24 + 1152 + 180 + 288 + 600) + 4 * nnz + 10 * m + 5 * n
+        return dict(form=form, scale=scale, fact=fact, iter=it, check=check, solve=it)
+    fma = 2
+    gj = 12 * 12 * 11 * fma + 12 * 4                     # 12x12 Gauss-Jordan (+ Newton reciprocal)
+    fact = N * (144 * 5 * fma                           # K_ff: B' R B on rows 6..11 + swing + friction
+                + gj                                    # F = K_ff^-1
+                + (3 * 4 + 3 * 12) * 12 * fma           # F W (rows 6..8 touch one force per foot)
+                + 36 * 12 * fma                         # Q = W' F W
+                + 12 * 30 * fma                         # D / L rows of the state block
+                + 2 * 12 * 12 * 7 * fma                 # coupling C S^-1 (seven-wide C) and its Schur update
+                + gj)                                   # S^-1 (or U^-1, M^-1)
+    # per stage: A_f' w (10 terms per force column), u = F b_f (12x12), beta = (F W)' b_f (6x12),
+    # the three sweep products (G y, S^-1 y, G' x: 12x12 each), the force recovery (F W) g (12x6),
+    # (R^-1 Q) g (6x6), A x~ on the 44 rows, the z / y / x updates
+    solve = N * ((12 * 10 + 144 + 72 + 3 * 144 + 72 + 36) * fma + 44 * 4)
+    it = solve + N * (44 * 8 + 24 * 3)
+    return dict(form=form, scale=scale, fact=fact, iter=it, check=check, solve=solve)
 
 
 def flops(N: int, iters, rho_updates, check_every: int = 25, adapt_every: int = 100,
-          scaling_iters: int = 10) -> np.ndarray:
-    """Per-instance algorithmic flops for measured iteration / rho-update counts."""
-    c = flops_components(N, scaling_iters)
+          scaling_iters: int = 10, polish_rounds=None, polish_solves: int = 11,
+          structured: bool = True) -> np.ndarray:
+    """Per-instance algorithmic flops for measured iteration / rho-update counts
+    (and, with polish, measured polish rounds: each one factorisation, 1 +
+    refinement KKT solves and a residual evaluation)."""
+    c = flops_components(N, scaling_iters, structured)
     K = np.asarray(iters, dtype=np.float64)
     R = np.asarray(rho_updates, dtype=np.float64)
     n_checks = np.floor(K / check_every)
     if adapt_every:
         n_checks += np.floor(K / adapt_every) - np.floor(K / np.lcm(check_every, adapt_every))
     n_checks += 1  # final evaluation when the loop exits on max_iter without a check
-    return c["form"] + c["scale"] + (1 + R) * c["fact"] + K * c["iter"] + n_checks * c["check"]
+    f = c["form"] + c["scale"] + (1 + R) * c["fact"] + K * c["iter"] + n_checks * c["check"]
+    if polish_rounds is not None:
+        P = np.asarray(polish_rounds, dtype=np.float64)
+        f = f + P * (c["fact"] + polish_solves * c["solve"] + c["check"])
+    return f
 
 
 def planner_bytes_per_instance(N: int, with_reduced: bool = True) -> int:

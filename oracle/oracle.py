@@ -79,31 +79,47 @@ def build(force: bool = False) -> str:
     return _LIB_PATH
 
 
-_lib = None
+_libs: dict = {}
+
+
+def _bind(path: str):
+    L = C.CDLL(path)
+    dp = C.POINTER(C.c_double)
+    ip = C.POINTER(C.c_int32)
+    L.oracle_default_params.argtypes = [C.POINTER(Params)]
+    L.oracle_pattern.argtypes = [C.c_int, ip, ip]
+    L.oracle_formulate.argtypes = [C.POINTER(Params), C.c_int, dp, dp, C.c_int, dp, dp, dp]
+    L.oracle_qp_solve.argtypes = [C.POINTER(Params), C.c_int, dp, dp, dp, dp, dp, dp,
+                                  dp, dp, ip, ip, dp, ip]
+    L.oracle_solve_batch.argtypes = [C.POINTER(Params), C.c_int, C.c_int64, dp, dp, C.c_int,
+                                     dp, dp, ip, ip, C.c_int]
+    L.oracle_num_threads.restype = C.c_int
+    L.oracle_default_planner_params.argtypes = [C.POINTER(PlannerParams)]
+    L.oracle_retrieve.argtypes = [C.POINTER(Params), C.c_int, dp, dp, dp, dp, dp, C.c_int,
+                                  dp, dp, dp, dp, dp, dp]
+    L.oracle_plan.argtypes = [C.POINTER(PlannerParams), C.c_int, C.c_uint, C.c_int, dp, dp, dp, dp, dp,
+                              C.c_int, dp, ip, dp, dp, dp]
+    return L
 
 
 def lib():
-    global _lib
-    if _lib is None:
+    """The checker build (-O2 -ffp-contract=off: the rounding the parity tests pin)."""
+    if "check" not in _libs:
         build()
-        L = C.CDLL(_LIB_PATH)
-        dp = C.POINTER(C.c_double)
-        ip = C.POINTER(C.c_int32)
-        L.oracle_default_params.argtypes = [C.POINTER(Params)]
-        L.oracle_pattern.argtypes = [C.c_int, ip, ip]
-        L.oracle_formulate.argtypes = [C.POINTER(Params), C.c_int, dp, dp, C.c_int, dp, dp, dp]
-        L.oracle_qp_solve.argtypes = [C.POINTER(Params), C.c_int, dp, dp, dp, dp, dp, dp,
-                                      dp, dp, ip, ip, dp, ip]
-        L.oracle_solve_batch.argtypes = [C.POINTER(Params), C.c_int, C.c_int64, dp, dp, C.c_int,
-                                         dp, dp, ip, ip, C.c_int]
-        L.oracle_num_threads.restype = C.c_int
-        L.oracle_default_planner_params.argtypes = [C.POINTER(PlannerParams)]
-        L.oracle_retrieve.argtypes = [C.POINTER(Params), C.c_int, dp, dp, dp, dp, dp, C.c_int,
-                                      dp, dp, dp, dp, dp, dp]
-        L.oracle_plan.argtypes = [C.POINTER(PlannerParams), C.c_int, C.c_uint, C.c_int, dp, dp, dp, dp, dp,
-                                  C.c_int, dp, ip, dp, dp, dp]
-        _lib = L
-    return _lib
+        _libs["check"] = _bind(_LIB_PATH)
+    return _libs["check"]
+
+
+def native_lib():
+    """A baseline build for THIS host (-O3 -march=native, contraction on), compiled
+    into a fresh temporary directory on first use so that a library built for
+    another CPU is never loaded.  Used only to time the CPU baseline."""
+    if "native" not in _libs:
+        import tempfile
+        out = os.path.join(tempfile.mkdtemp(prefix="mpcq_oracle_"), "liboracle_native.so")
+        subprocess.run(["make", "-s", "-C", _HERE, f"NATIVE_OUT={out}", "native"], check=True)
+        _libs["native"] = _bind(out)
+    return _libs["native"]
 
 
 def default_params(**overrides) -> Params:
@@ -173,8 +189,9 @@ def qp_solve(N, Ax, l, u, params: Params | None = None, warm_x=None, warm_y=None
 
 
 def solve_batch(xref, fsteps, mode: int = 0, params: Params | None = None, nthreads: int = 0,
-                want_x: bool = False):
-    """Batched formulation + solve on host threads (OpenMP)."""
+                want_x: bool = False, native: bool = False):
+    """Batched formulation + solve on host threads (OpenMP); native=True runs the
+    -O3 -march=native baseline build (timing only)."""
     xref = np.ascontiguousarray(xref, np.float64)
     fsteps = np.ascontiguousarray(fsteps, np.float64)
     B = xref.shape[0]
@@ -185,8 +202,8 @@ def solve_batch(xref, fsteps, mode: int = 0, params: Params | None = None, nthre
     st = np.zeros(B, np.int32)
     it = np.zeros(B, np.int32)
     p = params or default_params()
-    lib().oracle_solve_batch(C.byref(p), N, B, _dp(xref), _dp(fsteps), mode, _dp(f0), _dp(x),
-                             _ip(st), _ip(it), nthreads)
+    (native_lib() if native else lib()).oracle_solve_batch(C.byref(p), N, B, _dp(xref), _dp(fsteps), mode,
+                                                          _dp(f0), _dp(x), _ip(st), _ip(it), nthreads)
     return dict(f0=f0, x=x, status=st, iters=it)
 
 

@@ -58,8 +58,10 @@ __global__ __launch_bounds__(64) void retrieve_kernel(SessionArgs a) {
   const double* gx = a.x + b * n;
   const double* xr = a.xref + b * 12 * NP;
   const int st = a.status[b];
+  // a robot whose planner failed this tick (where the reference raises) is treated
+  // like a failed solve: it keeps its pose and virtual state and restarts cold
   const bool failed = !(st == MPCQ_STATUS_SOLVED || st == MPCQ_STATUS_SOLVED_INACCURATE ||
-                        st == MPCQ_STATUS_MAX_ITER_REACHED);
+                        st == MPCQ_STATUS_MAX_ITER_REACHED) || a.plan_status[b] != 0;
   for (int e = lane; e < n; e += 64) {
     const double v = gx[e];
     xs[e] = v;

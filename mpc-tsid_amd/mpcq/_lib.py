@@ -4,11 +4,14 @@ The shared library is built in-tree (mpc-tsid_amd/csrc/Makefile ->
 mpc-tsid_amd/mpcq/libmpcq.so) and loaded from here.  There is no fallback:
 if the library or a HIP device is missing, the calls raise.
 
-A process that also uses torch.cuda (device-pointer entry points on torch
-tensors) must ``import torch`` before the first call here: torch bundles its
-own HIP runtime, and libmpcq.so then binds to it (same sonames).  Loaded the
-other way round, two runtimes end up in the process and torch sees no device
-(tools/diag_runtime.py).
+torch bundles its own HIP runtime (torch/lib/libamdhip64.so, soname
+libamdhip64.so.7, the same as /opt/rocm's).  If libmpcq.so were loaded first
+it would bind /opt/rocm's copy, torch would load its own next to it, and two
+runtimes in one process leave torch without a device (tools/diag_runtime.py).
+So before loading libmpcq.so this module loads the HIP runtime torch will use
+(torch's own copy, found without importing torch) with RTLD_GLOBAL: libmpcq.so
+binds to it whatever the import order, and there is one runtime per process.
+Without torch installed, /opt/rocm's runtime is used.
 """
 from __future__ import annotations
 
@@ -17,10 +20,12 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# MPCQ_LIB_VARIANT=stamps loads the diagnostic build (per-phase cycle stamps)
-# (any other MPCQ_LIB_VARIANT=<v> loads libmpcq_<v>.so, an experiment build)
+# MPCQ_LIB_VARIANT=stamps loads the diagnostic build of the same Makefile
+# (per-phase cycle stamps, tools/stamps.py); no other variant exists
 _VARIANT = os.environ.get("MPCQ_LIB_VARIANT")
-LIB_PATH = os.path.join(HERE, f"libmpcq_{_VARIANT}.so" if _VARIANT else "libmpcq.so")
+if _VARIANT not in (None, "", "stamps"):
+    raise ImportError(f"MPCQ_LIB_VARIANT={_VARIANT!r}: only 'stamps' (the diagnostic build) exists")
+LIB_PATH = os.path.join(HERE, "libmpcq_stamps.so" if _VARIANT else "libmpcq.so")
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 
 # return codes / status / flags / modes (include/mpcq.h)
@@ -121,6 +126,32 @@ def build(force: bool = False) -> str:
 
 
 _lib = None
+_hip_runtime = None
+
+
+def hip_runtime_path():
+    """The libamdhip64 this process uses: torch's bundled copy when torch is
+    installed (whether or not it is imported yet), else the system one."""
+    import importlib.util
+    import sys
+    t = sys.modules.get("torch")
+    base = os.path.dirname(t.__file__) if t is not None and getattr(t, "__file__", None) else None
+    if base is None:
+        spec = importlib.util.find_spec("torch")
+        base = os.path.dirname(spec.origin) if spec is not None and spec.origin else None
+    if base is not None:
+        cand = os.path.join(base, "lib", "libamdhip64.so")
+        if os.path.exists(cand):
+            return cand
+    return None
+
+
+def _preload_hip_runtime():
+    global _hip_runtime
+    if _hip_runtime is None:
+        path = hip_runtime_path()
+        _hip_runtime = C.CDLL(path, mode=C.RTLD_GLOBAL) if path else False
+    return _hip_runtime
 
 
 def lib():
@@ -129,6 +160,7 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise MpcqError(E_DEVICE, f"{LIB_PATH} is missing: run `make -C {CSRC}` (or __graft_entry__.build())")
+    _preload_hip_runtime()
     L = C.CDLL(LIB_PATH)
     dp, ip, vp = C.POINTER(C.c_double), C.POINTER(C.c_int32), C.c_void_p
     PP = C.POINTER(Params)

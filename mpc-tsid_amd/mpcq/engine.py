@@ -17,6 +17,7 @@ so callers can keep inputs resident in HBM and time the kernel alone.
 from __future__ import annotations
 
 import ctypes as C
+import threading
 
 import numpy as np
 
@@ -59,14 +60,23 @@ class Engine:
         for k, v in overrides.items():
             setattr(self.params, k, v)
         self.n, self.m, self.nnz = dims(self.n_steps)
+        self.lock = threading.RLock()
         h = C.c_void_p()
         L.check(L.lib().mpcq_create(self.device, self.n_steps, C.byref(self.params), C.byref(h)))
         self._h = h
 
+    def _call(self, name: str, *args):
+        """One C-ABI call on this context.  A context is used by one host thread at a
+        time (include/mpcq.h): the lock serialises callers that share the Engine
+        (the asynchronous MPC_Wrapper's worker and the caller's thread)."""
+        with self.lock:
+            return L.check(getattr(L.lib(), name)(*args))
+
     def close(self):
         if getattr(self, "_h", None):
-            L.lib().mpcq_destroy(self._h)
-            self._h = None
+            with self.lock:
+                L.lib().mpcq_destroy(self._h)
+                self._h = None
 
     def __del__(self):
         try:
@@ -100,8 +110,8 @@ class Engine:
         l = np.empty((B, self.m))
         u = np.empty((B, self.m))
         st = np.empty(B, np.int32)
-        L.check(L.lib().mpcq_formulate_batch(self._h, B, _p(xref), _p(fsteps), mode, _p(Ax), _p(l), _p(u),
-                                             _p(st), 0))
+        self._call("mpcq_formulate_batch", self._h, B, _p(xref), _p(fsteps), mode, _p(Ax), _p(l), _p(u),
+                                             _p(st), 0)
         return dict(Ax=Ax, l=l, u=u, status=st)
 
     def qp_solve(self, Ax, l, u, warm_x=None, warm_y=None, rho=None, want_y: bool = True):
@@ -119,8 +129,8 @@ class Engine:
         it = np.empty(B, np.int32)
         ro = np.empty(B)
         info = np.empty((B, 4), np.int32)
-        L.check(L.lib().mpcq_qp_solve_batch(self._h, B, _p(Ax), _p(l), _p(u), _p(wx), _p(wy), _p(rho_in),
-                                            _p(x), _p(y), _p(st), _p(it), _p(ro), _p(info), 0))
+        self._call("mpcq_qp_solve_batch", self._h, B, _p(Ax), _p(l), _p(u), _p(wx), _p(wy), _p(rho_in),
+                                            _p(x), _p(y), _p(st), _p(it), _p(ro), _p(info), 0)
         return dict(x=x, y=y, status=st, iters=it, rho=ro, rho_updates=info[:, 0], polish=info[:, 1])
 
     def solve(self, xref, fsteps, mode: int = L.MODE_UPDATE, warm_x=None, warm_y=None,
@@ -134,8 +144,8 @@ class Engine:
         st = np.empty(B, np.int32)
         it = np.empty(B, np.int32)
         info = np.empty((B, 4), np.int32)
-        L.check(L.lib().mpcq_solve_batch(self._h, B, _p(xref), _p(fsteps), mode, _p(wx), _p(wy), _p(f0),
-                                         _p(x), _p(y), _p(st), _p(it), _p(info), 0))
+        self._call("mpcq_solve_batch", self._h, B, _p(xref), _p(fsteps), mode, _p(wx), _p(wy), _p(f0),
+                                         _p(x), _p(y), _p(st), _p(it), _p(info), 0)
         return dict(f0=f0, x=x, y=y, status=st, iters=it, rho_updates=info[:, 0], polish=info[:, 1])
 
     # ------------------------------------------------------------------ footstep planner
@@ -163,9 +173,9 @@ class Engine:
                 raise ValueError(f"{name} must be a C-contiguous {np.dtype(dt).name} array of shape {shp}")
         st = np.empty(B, np.int32)
         pp = params if params is not None else L.default_planner_params(dt=self.params.dt)
-        L.check(L.lib().mpcq_plan_batch(self._h, C.byref(pp), B, ops, int(k), _p(state), _p(v_cur), _p(h),
+        self._call("mpcq_plan_batch", self._h, C.byref(pp), B, ops, int(k), _p(state), _p(v_cur), _p(h),
                                         _p(l_feet), _p(v_ref), _p(red), _p(gait), _p(rot_flag), _p(h_rot),
-                                        _p(xref), _p(fsteps), _p(st), 0))
+                                        _p(xref), _p(fsteps), _p(st), 0)
         return st
 
     def plan_device(self, batch: int, ops: int, k: int, state_ptr: int, l_feet_ptr: int, v_ref_ptr: int,
@@ -175,14 +185,14 @@ class Engine:
         flags = L.FLAG_DEVICE_PTRS | (L.FLAG_ASYNC if asynchronous else 0)
         v = lambda q: C.c_void_p(q) if q else None  # noqa: E731
         pp = params if params is not None else L.default_planner_params(dt=self.params.dt)
-        L.check(L.lib().mpcq_plan_batch(self._h, C.byref(pp), int(batch), ops, int(k), v(state_ptr), v(v_cur_ptr),
+        self._call("mpcq_plan_batch", self._h, C.byref(pp), int(batch), ops, int(k), v(state_ptr), v(v_cur_ptr),
                                         v(h_ptr), v(l_feet_ptr), v(v_ref_ptr), v(reduced_ptr), v(gait_ptr),
                                         v(rot_flag_ptr), v(h_rot_ptr), v(xref_ptr), v(fsteps_ptr), v(status_ptr),
-                                        flags))
+                                        flags)
 
     # ------------------------------------------------------------------ device pointers
     def set_stream(self, stream_handle: int | None):
-        L.check(L.lib().mpcq_set_stream(self._h, C.c_void_p(stream_handle or 0)))
+        self._call("mpcq_set_stream", self._h, C.c_void_p(stream_handle or 0))
 
     def solve_device(self, batch: int, xref_ptr: int, fsteps_ptr: int, f0_ptr: int, status_ptr: int,
                      iters_ptr: int = 0, x_ptr: int = 0, y_ptr: int = 0, mode: int = L.MODE_UPDATE,
@@ -190,12 +200,12 @@ class Engine:
                      asynchronous: bool = False):
         flags = L.FLAG_DEVICE_PTRS | (L.FLAG_ASYNC if asynchronous else 0)
         v = lambda q: C.c_void_p(q) if q else None  # noqa: E731
-        L.check(L.lib().mpcq_solve_batch(self._h, int(batch), v(xref_ptr), v(fsteps_ptr), mode, v(warm_x_ptr),
+        self._call("mpcq_solve_batch", self._h, int(batch), v(xref_ptr), v(fsteps_ptr), mode, v(warm_x_ptr),
                                          v(warm_y_ptr), v(f0_ptr), v(x_ptr), v(y_ptr), v(status_ptr),
-                                         v(iters_ptr), v(info_ptr), flags))
+                                         v(iters_ptr), v(info_ptr), flags)
 
     def last_kernel_ms(self):
         f = C.c_double()
         s = C.c_double()
-        L.check(L.lib().mpcq_last_kernel_ms(self._h, C.byref(f), C.byref(s)))
+        self._call("mpcq_last_kernel_ms", self._h, C.byref(f), C.byref(s))
         return f.value, s.value

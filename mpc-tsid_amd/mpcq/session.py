@@ -46,8 +46,8 @@ class Session:
         if gait0 is not None:
             g = np.ascontiguousarray(np.broadcast_to(np.asarray(gait0, np.float64), (self.batch, 20, 5)))
         h = C.c_void_p()
-        L.check(L.lib().mpcq_session_create(engine._h, self.batch, C.byref(self.planner_params),
-                                            None if g is None else C.c_void_p(g.ctypes.data), C.byref(h)))
+        self.engine._call("mpcq_session_create", engine._h, self.batch, C.byref(self.planner_params),
+                                            None if g is None else C.c_void_p(g.ctypes.data), C.byref(h))
         self._h = h
         self.k = 0
 
@@ -83,7 +83,7 @@ class Session:
         lf = self._in(l_feet, (B, 3, 4))
         rd = self._in(reduced, (B,), np.int32)
         p = lambda a: None if a is None else C.c_void_p(a.ctypes.data)  # noqa: E731
-        L.check(L.lib().mpcq_session_tick(self._h, k, p(st), p(lf), p(vr), p(rd), 0))
+        self.engine._call("mpcq_session_tick", self._h, k, p(st), p(lf), p(vr), p(rd), 0)
         self.k = k + 1
         return self.read(L.SV_F0)
 
@@ -93,22 +93,22 @@ class Session:
         k = self.k if k is None else int(k)
         v = lambda q: C.c_void_p(q) if q else None  # noqa: E731
         flags = L.FLAG_DEVICE_PTRS | (L.FLAG_ASYNC if asynchronous else 0)
-        L.check(L.lib().mpcq_session_tick(self._h, k, v(state_ptr), v(l_feet_ptr), v(v_ref_ptr), v(reduced_ptr),
-                                          flags))
+        self.engine._call("mpcq_session_tick", self._h, k, v(state_ptr), v(l_feet_ptr), v(v_ref_ptr), v(reduced_ptr),
+                                          flags)
         self.k = k + 1
 
     def read(self, what: int):
         shape, dt = self._shapes[what]
         out = np.empty(shape, dt)
-        L.check(L.lib().mpcq_session_read(self._h, what, C.c_void_p(out.ctypes.data), 0))
+        self.engine._call("mpcq_session_read", self._h, what, C.c_void_p(out.ctypes.data), 0)
         return out
 
     def write(self, what: int, value):
         shape, dt = self._shapes[what]
         a = np.ascontiguousarray(np.broadcast_to(np.asarray(value, dt), shape))
-        L.check(L.lib().mpcq_session_write(self._h, what, C.c_void_p(a.ctypes.data), 0))
+        self.engine._call("mpcq_session_write", self._h, what, C.c_void_p(a.ctypes.data), 0)
 
     def device_ptr(self, what: int) -> int:
         out = C.c_void_p()
-        L.check(L.lib().mpcq_session_device_ptr(self._h, what, C.byref(out)))
+        self.engine._call("mpcq_session_device_ptr", self._h, what, C.byref(out))
         return int(out.value or 0)

@@ -160,12 +160,26 @@ class MPC_Wrapper:
         self.not_first_iter = False
         self.k_mpc = k_mpc
         self.multiprocessing = multiprocessing
-        self.mpc = MPC(dt, n_steps, T_gait, device=device, engine=engine, **overrides)
+        self._mpc = MPC(dt, n_steps, T_gait, device=device, engine=engine, **overrides)
         self._pool = None
         self._pending = None
         if multiprocessing:
             from concurrent.futures import ThreadPoolExecutor
             self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="mpcq-async")
+
+    @property
+    def mpc(self):
+        """The MPC object whose attributes Logger / utils read (f_applied, x, x_robot,
+        q_w, ...): a tick still running on the worker is waited for first (without
+        consuming its result), so readers never see a half-updated object."""
+        self._settle()
+        return self._mpc
+
+    def _settle(self):
+        fut = self._pending
+        if fut is not None and not fut.done():
+            from concurrent.futures import wait
+            wait([fut])
 
     def solve(self, k, fstep_planner):
         if self.multiprocessing:
@@ -179,9 +193,11 @@ class MPC_Wrapper:
         fs[np.isnan(fs)] = 0.0  # MPC_Wrapper.py:222
         xref, fsteps = np.array(fstep_planner.xref, copy=True), np.array(fs, copy=True)
 
+        mpc = self._mpc
+
         def job():
-            self.mpc.run(k / self.k_mpc, xref, fsteps)
-            return self.mpc.f_applied.copy()
+            mpc.run(k / self.k_mpc, xref, fsteps)
+            return mpc.f_applied.copy()
 
         self._pending = self._pool.submit(job)
         return 0
@@ -222,7 +238,7 @@ class MPC_Wrapper:
     def solve_batch(self, xref, fsteps, mode: int = L.MODE_UPDATE, want_x: bool = False):
         """Batched hot path: B independent ticks (cold-started OSQP solves) -> f0 (B, 12).
         Returns (f0, info) with info = dict(status, iters, x)."""
-        r = self.mpc.engine.solve(xref, fsteps, mode, want_x=want_x)
+        r = self.mpc.engine.solve(xref, fsteps, mode, want_x=want_x)  # after any pending tick
         return r["f0"], dict(status=r["status"], iters=r["iters"], x=r["x"])
 
 

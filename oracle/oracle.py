@@ -302,7 +302,7 @@ class Session:
             r = qp_solve(N, Ax, l, u, self.p, warm_x=self.warm_x, warm_y=self.y, rho=self.rho)
         self.x, self.y, self.rho = r["x"], r["y"], r["rho"]
         self.status, self.iters = r["status"], r["iters"]
-        failed = self.status not in (1, 2, -2)
+        failed = self.status not in (1, 2, -2) or pst != 0  # a planner failure also keeps the pose
         o = retrieve(N, self.x, self.planner.xref, self.planner.fsteps, self.planner.gait, self.q_w, failed,
                      self.p, self.planner.p.shoulders[:])
         self.x_robot, self.cost, self.warm_x = o["x_robot"], o["cost"], o["warm_x"]

@@ -5,15 +5,6 @@ import sys
 import numpy as np
 import pytest
 
-# One HIP runtime per process: torch ships its own libamdhip64 / libhsa-runtime64.
-# Imported first, they also serve libmpcq.so (same sonames); loaded after
-# libmpcq.so has pulled in /opt/rocm's copies, torch finds no device
-# (tools/diag_runtime.py).  The device-pointer tests use torch tensors.
-try:
-    import torch  # noqa: F401
-except ImportError:  # pragma: no cover
-    torch = None
-
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "mpc-tsid_amd")
 for p in (REPO, PKG):

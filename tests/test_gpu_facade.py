@@ -86,3 +86,26 @@ def test_async_wrapper_matches_sync(golden16):
         ws.solve(20 * tick, Planner(golden16["xref"][b], golden16["fsteps"][b]))
         assert np.array_equal(wa.get_latest_result(), ws.get_latest_result())
     wa.close()
+
+
+def test_async_wrapper_shares_engine_safely(golden16):
+    """A batched solve and attribute reads while an asynchronous tick is in flight
+    on the same context: the context lock serialises the calls, reads wait for the
+    tick, and both results equal the ones computed without overlap."""
+    from mpcq.wrapper import MPC_Wrapper
+    wa = MPC_Wrapper(0.02, 16, 20, 0.32, multiprocessing=True, device=0)
+    ws = MPC_Wrapper(0.02, 16, 20, 0.32, device=0)
+    wa.get_latest_result()
+    ws.get_latest_result()
+    xb, fb = golden16["xref"][:32], golden16["fsteps"][:32]
+    ref_batch, _ = ws.solve_batch(xb, fb)
+    for tick in range(3):
+        b = tick % 3
+        wa.solve(20 * tick, Planner(golden16["xref"][b], golden16["fsteps"][b]))
+        f_batch, _ = wa.solve_batch(xb, fb)          # issued while the tick may still run
+        xr = wa.mpc.x_robot.copy()                   # waits for the tick
+        ws.solve(20 * tick, Planner(golden16["xref"][b], golden16["fsteps"][b]))
+        assert np.array_equal(f_batch, ref_batch)
+        assert np.array_equal(wa.get_latest_result(), ws.get_latest_result())
+        assert np.array_equal(xr, ws.mpc.x_robot)
+    wa.close()

@@ -6,6 +6,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 FORM_TOL = 1e-13  # formulation (relative, ulp-level: FMA contraction on the GPU)
+X_TOL = 1e-9      # GPU vs oracle solutions (same algorithm, same data; observed 1.5e-11)
 
 
 @pytest.fixture(scope="module")
@@ -68,7 +69,7 @@ def test_bad_gait_status(eng16, golden16, mpcq):
 @pytest.mark.parametrize("N", [16, 32])
 def test_qp_solve_vs_oracle(N, eng16, eng32, golden16, golden32, oracle):
     """Same OSQP-0.6 algorithm on the same QP data: statuses and iteration
-    counts agree and the returned forces agree far inside 1e-4."""
+    counts identical on every instance, x within X_TOL (observed 1.5e-11)."""
     e, g = (eng16, golden16) if N == 16 else (eng32, golden32)
     r = e.qp_solve(g["Ax"], g["l"], g["u"])
     B = g["Ax"].shape[0]
@@ -82,9 +83,8 @@ def test_qp_solve_vs_oracle(N, eng16, eng32, golden16, golden32, oracle):
     errs = np.array(errs)
     print(f"N={N}: iteration counts equal on {same_it}/{B}; max|x-x_oracle| {errs.max():.2e} "
           f"median {np.median(errs):.2e}; iters {np.median(r['iters'])}")
-    assert same_it >= 0.9 * B
-    assert np.median(errs) < 1e-6
-    assert errs.max() < 1e-4
+    assert same_it == B
+    assert errs.max() < X_TOL
 
 
 def test_fused_vs_oracle(eng16, oracle, mpcq):
@@ -92,10 +92,69 @@ def test_fused_vs_oracle(eng16, oracle, mpcq):
     r = eng16.solve(b["xref"], b["fsteps"], 0)
     o = oracle.solve_batch(b["xref"], b["fsteps"], 0, nthreads=8)
     assert np.array_equal(r["status"], o["status"])
+    assert np.array_equal(r["iters"], o["iters"])
     err = np.abs(r["f0"] - o["f0"]).max(axis=1)
     print(f"fused: max|f0-f0_oracle| {err.max():.2e} median {np.median(err):.2e}")
-    assert np.median(err) < 1e-6
-    assert err.max() < 1e-4
+    assert err.max() < X_TOL
+
+
+def _certified(xref, fsteps, x, y):
+    from oracle import certify
+    fstar, kkt, ok = certify.certified_forces(xref, fsteps, x, y)
+    assert ok.all(), kkt.max()
+    return fstar
+
+
+def test_headline_c2_full_batch(mpcq, oracle):
+    """BASELINE C2 exactly as bench.py runs it (1024 instances, seed 2, trot, polish on):
+    every instance solved, statuses / iteration counts / polish outcome equal to the
+    oracle's on every instance, forces within 1e-6 of each QP's KKT-certified optimum
+    (observed 3.3e-10) and within X_TOL of the oracle's polished forces."""
+    from mpcq import shard
+    b = shard.shard_batch(1024, 1, 0, 16, ("trot",), seed=2)
+    over = dict(polish=2, polish_rounds=8, polish_refine_iter=10)
+    with mpcq.Engine(16, **over) as e:
+        r = e.solve(b["xref"], b["fsteps"], 0, want_y=True)
+    assert (r["status"] == mpcq.STATUS_SOLVED).all()
+    o = oracle.solve_batch(b["xref"], b["fsteps"], 0, params=oracle.default_params(**over), nthreads=16)
+    assert np.array_equal(r["status"], o["status"])
+    assert np.array_equal(r["iters"], o["iters"])
+    assert (r["polish"] == 1).all()
+    fstar = _certified(b["xref"], b["fsteps"], r["x"], r["y"])
+    d_star = np.abs(r["f0"] - fstar).max()
+    d_ora = np.abs(r["f0"] - o["f0"]).max()
+    print(f"C2 full batch: max|f0 - f0*| {d_star:.2e}, max|f0 - f0_oracle| {d_ora:.2e}, "
+          f"iters median {np.median(r['iters'])} max {r['iters'].max()}")
+    assert d_star < 1e-6
+    assert d_ora < X_TOL
+
+
+def test_admm_c2_full_batch_vs_oracle(eng16, mpcq, oracle):
+    """C2 with polish off (the reference's own settings): statuses and iteration
+    counts equal to the oracle's on all 1024 instances; the two-instances-per-CU,
+    two-round schedule of the full launch changes nothing."""
+    from mpcq import shard
+    b = shard.shard_batch(1024, 1, 0, 16, ("trot",), seed=2)
+    r = eng16.solve(b["xref"], b["fsteps"], 0)
+    o = oracle.solve_batch(b["xref"], b["fsteps"], 0, nthreads=16)
+    assert np.array_equal(r["status"], o["status"])
+    assert np.array_equal(r["iters"], o["iters"])
+    assert np.abs(r["f0"] - o["f0"]).max() < X_TOL
+
+
+def test_c5_size_launch(eng16, mpcq, oracle):
+    """A C5-sized launch (32768 mixed-gait instances, 64 rounds of the grid): every
+    instance solved; a strided sample of 512 equals the oracle (status, iterations,
+    forces within X_TOL)."""
+    from mpcq import shard
+    b = shard.shard_batch(32768, 1, 0, 16, ("trot", "bound", "pace"), seed=5)
+    r = eng16.solve(b["xref"], b["fsteps"], 0, want_x=False)
+    assert np.isin(r["status"], (1, 2)).all(), np.unique(r["status"], return_counts=True)
+    sel = np.arange(0, 32768, 64)
+    o = oracle.solve_batch(b["xref"][sel], b["fsteps"][sel], 0, nthreads=16)
+    assert np.array_equal(r["status"][sel], o["status"])
+    assert np.array_equal(r["iters"][sel], o["iters"])
+    assert np.abs(r["f0"][sel] - o["f0"]).max() < X_TOL
 
 
 def test_nonfinite_input(eng16, golden16, mpcq):

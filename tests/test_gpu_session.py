@@ -4,15 +4,17 @@ robot and tick by tick, on identical inputs.
 
 Tolerances: gait / rotation flag exact; xref, fsteps within 1e-15 (cos/sin
 ulps) when the states come from the host, within SOLVE_TOL on the virtual
-robot (whose states are solver outputs); forces and solutions within SOLVE_TOL (the ADMM iterates follow the
-oracle's to ~1e-11, BASELINE.json's bar is 1e-4); status identical; iteration
-counts identical on >= 90 % of (robot, tick) pairs."""
+robot (whose states are solver outputs); forces and solutions within SOLVE_TOL
+(observed 1.3e-9 after 10 warm-started ticks; the tolerance sits two decades
+above; the virtual robot's states, fed back from the solutions, also get a
+relative 1e-6); status and iteration counts identical on every (robot, tick)
+pair."""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
-SOLVE_TOL = 1e-6
+SOLVE_TOL = 1e-7
 
 
 @pytest.fixture(scope="module")
@@ -36,7 +38,7 @@ def _inputs(rng, B, k):
     return state, l_feet, v_ref
 
 
-def _compare(sess, ors, mpcq, k, agree, plan_tol=1e-15):
+def _compare(sess, ors, mpcq, k, agree, plan_tol=1e-15, x_rtol=0.0):
     B = len(ors)
     f0 = sess.read(mpcq.SV_F0)
     st = sess.read(mpcq.SV_STATUS)
@@ -56,9 +58,9 @@ def _compare(sess, ors, mpcq, k, agree, plan_tol=1e-15):
         assert np.array_equal(np.isnan(fs[b]), np.isnan(o.planner.fsteps)), ctx
         np.testing.assert_allclose(np.nan_to_num(fs[b]), np.nan_to_num(o.planner.fsteps), rtol=0, atol=plan_tol)
         np.testing.assert_allclose(f0[b], o.f0, rtol=0, atol=SOLVE_TOL, err_msg=str(ctx))
-        np.testing.assert_allclose(x[b], o.x, rtol=0, atol=SOLVE_TOL, err_msg=str(ctx))
-        np.testing.assert_allclose(xr[b], o.x_robot, rtol=0, atol=SOLVE_TOL, err_msg=str(ctx))
-        np.testing.assert_allclose(qw[b], o.q_w, rtol=0, atol=SOLVE_TOL, err_msg=str(ctx))
+        np.testing.assert_allclose(x[b], o.x, rtol=x_rtol, atol=SOLVE_TOL, err_msg=str(ctx))
+        np.testing.assert_allclose(xr[b], o.x_robot, rtol=x_rtol, atol=SOLVE_TOL, err_msg=str(ctx))
+        np.testing.assert_allclose(qw[b], o.q_w, rtol=x_rtol, atol=SOLVE_TOL, err_msg=str(ctx))
         np.testing.assert_allclose(cost[b], o.cost, rtol=1e-6, atol=1e-12, err_msg=str(ctx))
         agree.append(it[b] == o.iters)
     return float(np.abs(f0 - np.stack([o.f0 for o in ors])).max()), it
@@ -82,7 +84,7 @@ def test_session_host_inputs_vs_oracle(mpcq, N):
                 o.tick(k, v_ref[b], state=state[b], l_feet=l_feet[b], reduced=bool(red[b]))
             d, _ = _compare(sess, ors, mpcq, k, agree)
             worst = max(worst, d)
-    assert np.mean(agree) >= 0.9
+    assert np.mean(agree) == 1.0
     print(f"N={N}: max |f0 - f0_oracle| over {T} ticks = {worst:.2e}, iteration counts agree {np.mean(agree):.3f}")
 
 
@@ -102,15 +104,16 @@ def test_session_virtual_robot_vs_oracle(mpcq):
             sess.tick(v_ref)
             for b, o in enumerate(ors):
                 o.tick(k, v_ref[b])
-            # the state fed to the planner is itself a solver output here
-            _, it = _compare(sess, ors, mpcq, k, agree, plan_tol=SOLVE_TOL)
+            # the state fed to the planner is itself a solver output here, so rounding
+            # differences compound over the ticks (observed 7.8e-7 on |x| ~ 5 after 9 ticks)
+            _, it = _compare(sess, ors, mpcq, k, agree, plan_tol=SOLVE_TOL, x_rtol=1e-6)
             its.append(it)
-            np.testing.assert_allclose(sess.read(mpcq.SV_STATE), np.stack([o.state for o in ors]), rtol=0,
+            np.testing.assert_allclose(sess.read(mpcq.SV_STATE), np.stack([o.state for o in ors]), rtol=1e-6,
                                        atol=SOLVE_TOL)
-            np.testing.assert_allclose(sess.read(mpcq.SV_L_FEET), np.stack([o.l_feet for o in ors]), rtol=0,
+            np.testing.assert_allclose(sess.read(mpcq.SV_L_FEET), np.stack([o.l_feet for o in ors]), rtol=1e-6,
                                        atol=SOLVE_TOL)
     its = np.array(its)
-    assert np.mean(agree) >= 0.9
+    assert np.mean(agree) == 1.0
     # warm starts (shifted x, y, rho carried over) cut the iterations after the first tick
     assert np.median(its[1:]) < np.median(its[0]), its.tolist()
 
@@ -135,14 +138,23 @@ def test_session_device_pointers_async(mpcq):
 
 
 def test_session_bad_gait_reported(mpcq):
+    """A robot whose gait table is malformed (the reference planner raises) reports
+    BAD_GAIT, keeps its pose and virtual state and restarts cold; the others walk."""
     N, B = 16, 4
     gaits = _gaits(B, N)
     gaits[2, :, 0] = 1.0  # no terminator: the reference planner raises
     with mpcq.Engine(N) as eng, mpcq.Session(eng, B, gait0=gaits) as sess:
-        sess.tick(np.tile([0.3, 0, 0, 0, 0, 0], (B, 1)))
-        st = sess.read(mpcq.SV_STATUS)
-        assert st[2] == mpcq.STATUS_BAD_GAIT
-        assert (np.delete(st, 2) == 1).all()
+        q0 = sess.read(mpcq.SV_Q_W)
+        s0 = sess.read(mpcq.SV_STATE)
+        for k in range(3):
+            sess.tick(np.tile([0.3, 0, 0, 0, 0, 0], (B, 1)), k=k)
+            st = sess.read(mpcq.SV_STATUS)
+            assert st[2] == mpcq.STATUS_BAD_GAIT
+            assert (np.delete(st, 2) == 1).all()
+        qw = sess.read(mpcq.SV_Q_W)
+        assert np.array_equal(qw[2], q0[2]) and np.array_equal(sess.read(mpcq.SV_STATE)[2], s0[2])
+        assert not sess.read(mpcq.SV_Y)[2].any() and sess.read(mpcq.SV_RHO)[2] == eng.params.rho
+        assert (np.abs(np.delete(qw - q0, 2, axis=0)).max(axis=1) > 0).all()  # the others moved
 
 
 def test_session_api_edges(mpcq):

@@ -63,6 +63,10 @@ def main():
     for k2, v2 in counters(os.path.join(src, "sq2", "run_counter_collection.csv"), a.kernel).items():
         if k2 != "SQ_WAVES":
             sq[k2] = v2
+    f64 = counters(os.path.join(src, "f64", "run_counter_collection.csv"), a.kernel)
+    # the counter passes replay the same launches: their kernel time is the trace's average
+    kern_ms = (sum(float(r["AverageNs"]) * int(r["Calls"]) for r in eng) /
+               max(1, sum(int(r["Calls"]) for r in eng)) / 1e6) if eng else None
 
     fk, wk = mean(fetch.get("FETCH_SIZE", [])), mean(write.get("WRITE_SIZE", []))
     traffic = None
@@ -99,15 +103,34 @@ def main():
             if name.startswith("SQ_WAIT") or name.startswith("SQ_ACTIVE_INST"):
                 extra += f", {100 * v / cyc:.1f} % of wave cycles" if cyc else ""
             lines.append(f"- {name}: {v:.4g}{extra}")
+    fp64_flops = None
+    if f64:
+        fma, add, mul = (mean(f64.get(n, [])) or 0.0 for n in
+                         ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64"))
+        trans = mean(f64.get("SQ_INSTS_VALU_TRANS_F64", [])) or 0.0
+        valu = mean(f64.get("SQ_INSTS_VALU", [])) or 0.0
+        fp64_flops = (2 * fma + add + mul) * 64  # lane-ops of fully populated waves (rocprof's FP64 FLOPS formula)
+        lines += ["", "## FP64 instruction counters (per launch, wave instructions)", ""]
+        for name in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                     "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_MFMA_F64"):
+            v = mean(f64.get(name, []))
+            if v is not None:
+                lines.append(f"- {name}: {v:.4g}" + (f" ({100 * v / valu:.1f} % of VALU)" if valu else ""))
+        lines.append(f"- FP64 flops issued = (2 FMA + ADD + MUL) x 64 = {fp64_flops:.4g} per launch"
+                     + (f" -> {fp64_flops / (kern_ms * 1e-3) / 1e12:.2f} TFLOP/s over the {kern_ms:.3f} ms launch"
+                        if kern_ms else ""))
+        lines.append(f"- (transcendental FP64: {trans * 64:.3g} lane-ops, not counted as flops)")
     open(os.path.join(dst, f"{a.tag}_summary.md"), "w").write("\n".join(lines) + "\n")
-    if traffic is not None:
+    if traffic is not None or fp64_flops is not None:
         path = os.path.join(dst, "pmc_traffic.json")
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             d = {}
         d[a.key] = {"bytes_per_launch": traffic, "fetch_kib": fk, "write_kib": wk, "tag": a.tag,
-                    "note": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section), separate --pmc passes"}
+                    "fp64_flops_per_launch": fp64_flops, "kernel_ms": kern_ms,
+                    "note": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section), separate --pmc passes; "
+                            "fp64 flops = (2 SQ_INSTS_VALU_FMA_F64 + ADD_F64 + MUL_F64) x 64 from their own pass"}
         json.dump(d, open(path, "w"), indent=1)
     print("\n".join(lines))
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 evidence for one bench configuration: kernel-trace stats, then the
 # HBM counters (FETCH_SIZE and WRITE_SIZE in separate passes, as the gfx950 TCC
-# slot budget requires) and one SQ pass.  Counters never share a run with
+# slot budget requires), two SQ passes and the FP64 instruction-count pass.  Counters never share a run with
 # --sys-trace / --runtime-trace.  Every GPU step has its own time limit and the
 # chain stops at the first failure.
 #   bash tools/profile.sh <tag> [bench args...]
@@ -19,7 +19,9 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU \
     --output-format csv -d $OUT/sq -o run -- $B > $OUT/sq.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES \
-    --output-format csv -d $OUT/sq2 -o run -- $B > $OUT/sq2.log 2>&1
+    --output-format csv -d $OUT/sq2 -o run -- $B > $OUT/sq2.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_MFMA_F64 \
+    --output-format csv -d $OUT/f64 -o run -- $B > $OUT/f64.log 2>&1
 rc=$?
 echo "profile rc=$rc" >> $OUT/trace.log
 exit $rc

@@ -418,8 +418,6 @@ struct Smem {
   double zero[72];          // zeros: masked coefficient reads point here instead of selecting
   int flag[4];
 };
-// two instances share a CU's 160 KB at N = 16
-static_assert(sizeof(Smem<16>) <= 160 * 1024 / 2, "Smem<16> must leave room for two workgroups per CU");
 
 // prologue aliases inside GH
 template <int N>
@@ -516,7 +514,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
   double bnd = 0.0;
   double lo_g[FUSED ? 1 : 3], hi_g[FUSED ? 1 : 3];
   if (t == 0) { sh.flag[0] = 0; sh.flag[1] = 0; sh.flag[2] = 0; sh.flag[3] = 0; }
-  if (t < 72) sh.zero[t] = 0.0;
+  for (int e = t; e < 72; e += T) sh.zero[e] = 0.0;  // N = 4: one wave of 64 lanes
   if (t < 12) sh.u.it.xs[0][t] = 0.0;  // X_0 slot (masked reads multiply it by zero)
 
   // ---------------------------------------------------------------- prologue
@@ -1791,27 +1789,21 @@ hipError_t launch_t(bool fused, bool solve, const mpcq_params& p, const LaunchAr
 
 }  // namespace
 
-bool horizon_supported(int N) { return N == 16 || N == 32; }
+// One translation unit per horizon (the Makefile compiles this file once per
+// N with -DMPCQ_ENGINE_N=N, in parallel); mpcq_dispatch.cpp picks the unit.
+#ifndef MPCQ_ENGINE_N
+#error "compile mpcq_engine.hip with -DMPCQ_ENGINE_N=<horizon> (see the Makefile)"
+#endif
+static_assert(MPCQ_ENGINE_N % 4 == 0 && MPCQ_ENGINE_N >= 4, "a wave64 holds four 16-lane stage rows");
+static_assert(sizeof(Smem<MPCQ_ENGINE_N>) <= 160 * 1024, "Smem<N> exceeds the CU's LDS");
+static_assert(MPCQ_ENGINE_N > 16 || sizeof(Smem<MPCQ_ENGINE_N>) <= 80 * 1024,
+              "Smem<N> must fit twice in a CU for N <= 16");
 
-int supported_horizons(int32_t* out, int cap) {
-  const int32_t hs[2] = {16, 32};
-  for (int i = 0; i < 2 && i < cap; ++i) out[i] = hs[i];
-  return 2;
-}
-
-hipError_t launch_formulate(int N, const mpcq_params& p, const LaunchArgs& a, hipStream_t s) {
-  if (a.batch <= 0) return hipSuccess;
-  if (N == 16) return launch_t<16>(true, false, p, a, s);
-  if (N == 32) return launch_t<32>(true, false, p, a, s);
-  return hipErrorInvalidValue;
-}
-
-hipError_t launch_solve(int N, bool fused, const mpcq_params& p, const LaunchArgs& a,
-                        hipStream_t s) {
-  if (a.batch <= 0) return hipSuccess;
-  if (N == 16) return launch_t<16>(fused, true, p, a, s);
-  if (N == 32) return launch_t<32>(fused, true, p, a, s);
-  return hipErrorInvalidValue;
+#define MPCQ_CAT_(a, b) a##b
+#define MPCQ_CAT(a, b) MPCQ_CAT_(a, b)
+hipError_t MPCQ_CAT(engine_launch_n, MPCQ_ENGINE_N)(bool fused, bool solve, const mpcq_params& p,
+                                                   const LaunchArgs& a, hipStream_t s) {
+  return launch_t<MPCQ_ENGINE_N>(fused, solve, p, a, s);
 }
 
 }  // namespace mpcq

@@ -83,6 +83,8 @@ hipError_t launch_retrieve(int N, const SessionArgs& a, hipStream_t s);
 // Launchers (mpcq_engine.hip).  Return hipError_t.
 hipError_t launch_formulate(int N, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);
 hipError_t launch_solve(int N, bool fused, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);
+// the horizons the engine is compiled for (mpcq_dispatch.cpp, Makefile)
+#define MPCQ_HORIZONS(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32)
 bool horizon_supported(int N);
 int supported_horizons(int32_t* out, int cap);
 

@@ -26,7 +26,7 @@ namespace {
 struct PlanShared {
   alignas(16) double gait[100];
   alignas(16) double fs[260];
-  double v6[33], v7[33];
+  double v6[64], v7[64];  // xref columns 1..N (N <= 63: one lane per column)
   // per phase i of compute_footsteps: cos / sin of the yaw at the phase start and
   // the displacement dx, dy (FootstepPlanner.py:329-343), one lane per phase
   double ph_c[20], ph_s[20], ph_dx[20], ph_dy[20];
@@ -294,7 +294,7 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
 
 hipError_t launch_plan(const mpcq_planner_params& pp, const PlanArgs& a, hipStream_t s) {
   if (a.batch <= 0) return hipSuccess;
-  if (a.N + 1 > 64 || a.N + 1 > 33) return hipErrorInvalidValue;
+  if (a.N < 1 || a.N + 1 > 64) return hipErrorInvalidValue;
   hipLaunchKernelGGL(planner_kernel, dim3((unsigned)a.batch), dim3(64), 0, s, pp, a);
   return hipGetLastError();
 }

@@ -147,9 +147,13 @@ __global__ __launch_bounds__(64) void retrieve_kernel(SessionArgs a) {
 
 hipError_t launch_retrieve(int N, const SessionArgs& a, hipStream_t s) {
   if (a.batch <= 0) return hipSuccess;
-  if (N == 16) hipLaunchKernelGGL(retrieve_kernel<16>, dim3((unsigned)a.batch), dim3(64), 0, s, a);
-  else if (N == 32) hipLaunchKernelGGL(retrieve_kernel<32>, dim3((unsigned)a.batch), dim3(64), 0, s, a);
-  else return hipErrorInvalidValue;
+  switch (N) {
+#define MPCQ_RET_CASE(NN) \
+    case NN: hipLaunchKernelGGL(retrieve_kernel<NN>, dim3((unsigned)a.batch), dim3(64), 0, s, a); break;
+    MPCQ_HORIZONS(MPCQ_RET_CASE)
+#undef MPCQ_RET_CASE
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -121,7 +121,7 @@ class PlannerParams(C.Structure):
 def build(force: bool = False) -> str:
     """Compile libmpcq.so for gfx950 with hipcc (csrc/Makefile)."""
     if force or not os.path.exists(LIB_PATH):
-        subprocess.run(["make", "-s", "-C", CSRC], check=True)
+        subprocess.run(["make", "-s", "-j8", "-C", CSRC], check=True)
     return LIB_PATH
 
 
@@ -228,6 +228,6 @@ def default_planner_params(**overrides) -> PlannerParams:
 
 
 def supported_horizons():
-    buf = (C.c_int32 * 8)()
-    n = lib().mpcq_supported_horizons(buf, 8)
-    return [buf[i] for i in range(min(n, 8))]
+    buf = (C.c_int32 * 64)()
+    n = lib().mpcq_supported_horizons(buf, 64)
+    return [buf[i] for i in range(min(n, 64))]

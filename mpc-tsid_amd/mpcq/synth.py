@@ -41,6 +41,16 @@ GAIT_MASKS = {
 GAITS = ("trot", "bound", "pace")
 
 
+def period_steps(n_steps: int) -> int:
+    """MPC steps per gait period for horizon n_steps: 16 (T_gait / dt at dt = 0.02)
+    when N is a whole number of such periods, else one period spanning the horizon
+    (the reference's N = n_periods T_gait / dt, FootstepPlanner.py:55, with
+    dt = T_gait / N, e.g. N = 8 at dt = 0.04; N = 24 = 3 periods of 8 is another
+    valid table, this one is the single-period choice)."""
+    p = int(round(T_GAIT / DT))
+    return p if n_steps % p == 0 else n_steps
+
+
 def gait_table(gait: str, n_steps: int) -> np.ndarray:
     """20x5 table: [duration, stance FL, FR, HL, HR] (FootstepPlanner.py:207-231)."""
     g = np.zeros((20, 5))
@@ -48,10 +58,12 @@ def gait_table(gait: str, n_steps: int) -> np.ndarray:
         g[0, 0] = n_steps
         g[0, 1:] = 1.0
         return g
-    half = int(0.5 * T_GAIT / DT)
+    if n_steps % 2 or n_steps < 4:
+        raise ValueError(f"horizon {n_steps}: a gait period is two half periods of >= 2 steps")
+    half = period_steps(n_steps) // 2
     n_periods = n_steps // (2 * half)
-    if n_periods * 2 * half != n_steps:
-        raise ValueError(f"horizon {n_steps} is not a whole number of {2 * half}-step gait periods")
+    if n_periods > 4:
+        raise ValueError(f"horizon {n_steps}: {n_periods} periods do not fit the 20-row table")
     masks = GAIT_MASKS[gait]
     for i in range(n_periods):
         g[4 * i:4 * i + 4, 0] = (1, half - 1, 1, half - 1)

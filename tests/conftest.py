@@ -37,3 +37,14 @@ def oracle():
     from oracle import oracle as O
     O.build()
     return O
+
+
+@pytest.fixture(scope="session")
+def golden_h():
+    """Fixtures at the other horizons (gen_golden.py horizons): {N: {field: array}}."""
+    d = np.load(os.path.join(GOLDEN, "golden_horizons.npz"))
+    out = {}
+    for N in d["horizons"]:
+        pre = f"n{int(N)}_"
+        out[int(N)] = {k[len(pre):]: d[k] for k in d.files if k.startswith(pre)}
+    return out

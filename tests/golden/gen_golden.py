@@ -1,6 +1,8 @@
 """Generate the committed golden fixtures (run in the build container only).
 
     python tests/golden/gen_golden.py            # writes tests/golden/golden_n16.npz, golden_n32.npz
+    python tests/golden/gen_golden.py horizons   # writes tests/golden/golden_horizons.npz
+                                                 # (N = 4, 8, 12, 20, 24, 28 and 48; keys n<N>_<field>)
 
 What it does, per instance:
 1. Inputs: seeded synthetic (xref, fsteps) from mpcq.synth (trot / bound /
@@ -264,7 +266,26 @@ def build(N: int, per_gait: int, seed: int, extra=True):
     return arrs
 
 
+HORIZONS = ((4, 2, 404), (8, 4, 808), (12, 2, 1212), (20, 2, 2020), (24, 4, 2424), (28, 2, 2828), (48, 1, 4848))
+
+
+def main_horizons():
+    """The other horizons the engine compiles (N = 4j <= 32) plus N = 48 (three
+    16-step periods at dt = 0.02: n_periods = 3 in FootstepPlanner.py:55)."""
+    out = {}
+    for N, per_gait, seed in HORIZONS:
+        arrs = build(N, per_gait, seed)
+        for k, v in arrs.items():
+            out[f"n{N}_{k}"] = v
+    path = os.path.join(HERE, "golden_horizons.npz")
+    np.savez_compressed(path, horizons=np.array([h[0] for h in HORIZONS]), **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "horizons":
+        main_horizons()
+        return
     for N, per_gait, seed in ((16, 16, 1234), (32, 4, 4321)):
         arrs = build(N, per_gait, seed)
         path = os.path.join(HERE, f"golden_n{N}.npz")

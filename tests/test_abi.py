@@ -74,7 +74,13 @@ def test_dims_and_pattern(mpcq, N, golden16, golden32):
 
 
 def test_supported_horizons(mpcq):
-    assert mpcq.supported_horizons() == [16, 32]
+    assert mpcq.supported_horizons() == [4, 8, 12, 16, 20, 24, 28, 32]
+
+
+@pytest.mark.parametrize("N", [4, 8, 12, 20, 24, 28, 48])
+def test_pattern_other_horizons(mpcq, N, golden_h):
+    indptr, indices = mpcq.pattern(N)
+    assert np.array_equal(indptr, golden_h[N]["indptr"]) and np.array_equal(indices, golden_h[N]["indices"])
 
 
 def test_errors_are_codes_not_crashes(mpcq):

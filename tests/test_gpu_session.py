@@ -66,7 +66,7 @@ def _compare(sess, ors, mpcq, k, agree, plan_tol=1e-15, x_rtol=0.0):
     return float(np.abs(f0 - np.stack([o.f0 for o in ors])).max()), it
 
 
-@pytest.mark.parametrize("N", [16, 32])
+@pytest.mark.parametrize("N", [8, 16, 24, 32])
 def test_session_host_inputs_vs_oracle(mpcq, N):
     """Measured states from the host each tick (the reference's interface)."""
     from oracle import oracle as O

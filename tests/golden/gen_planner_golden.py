@@ -58,12 +58,13 @@ MASKS = {
 }
 
 
-def table(kind: str, n_periods: int, rng) -> np.ndarray:
+def table(kind: str, n_periods: int, rng, dt: float = 0.02) -> np.ndarray:
     g = np.zeros((20, 5))
-    N = 16 * n_periods
+    half = int(0.5 * 0.32 / dt)  # as create_walking_trot (FootstepPlanner.py:193-214)
+    N = 2 * half * n_periods
     if kind in MASKS:
         for i in range(n_periods):
-            g[4 * i:4 * i + 4, 0] = (1, 7, 1, 7)
+            g[4 * i:4 * i + 4, 0] = (1, half - 1, 1, half - 1)
             g[4 * i:4 * i + 4, 1:] = MASKS[kind]
     elif kind == "random":
         # random phases (durations sum to N), random contact masks, repeated masks allowed
@@ -99,11 +100,11 @@ def draw_inputs(rng, tick):
     return lC, abg, lV, lW, l_feet, v_ref, reduced
 
 
-def run_scenario(FP, kind: str, n_periods: int, seed: int):
+def run_scenario(FP, kind: str, n_periods: int, seed: int, dt: float = 0.02):
     rng = np.random.default_rng(seed)
-    pl = FP.FootstepPlanner(0.02, n_periods)
+    pl = FP.FootstepPlanner(dt, n_periods)
     if kind != "trot":
-        pl.gait = table(kind, n_periods, rng)
+        pl.gait = table(kind, n_periods, rng, dt)
     N = pl.n_steps
     rec = {k: [] for k in ("state", "l_feet", "v_ref", "reduced", "gait", "fsteps", "xref", "flag", "h_rot")}
     gait0 = pl.gait.copy()
@@ -145,6 +146,14 @@ def main():
         for kind in kinds:
             N, out = run_scenario(FP, kind, n_periods, seed=5000 + sid)
             sid += 1
+            groups.setdefault(N, []).append((kind, out))
+    # other horizons: dt = 0.04 (N = 8 per period: n_periods 1 and 3 -> N = 8, 24) and
+    # three periods at dt = 0.02 (N = 48); keys n<N>_*, the N = 16 / 32 ones unchanged
+    for dt, n_periods in ((0.04, 1), (0.04, 3), (0.02, 3)):
+        for kind in ("trot", "bound", "random", "static"):
+            N, out = run_scenario(FP, kind, n_periods, seed=7000 + sid, dt=dt)
+            sid += 1
+            out["dt"] = np.float64(dt)
             groups.setdefault(N, []).append((kind, out))
     arrs = {}
     for N, lst in groups.items():

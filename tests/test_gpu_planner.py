@@ -25,7 +25,7 @@ def mpcq():
 
 @pytest.fixture(scope="module")
 def engines(mpcq):
-    es = {N: mpcq.Engine(N) for N in (16, 32)}
+    es = {N: mpcq.Engine(N) for N in (8, 16, 24, 32)}
     yield es
     for e in es.values():
         e.close()
@@ -40,9 +40,9 @@ class BatchState:
         self.xref = np.zeros((B, 12, N + 1))
         self.fsteps = np.full((B, 20, 13), np.nan)
 
-    def plan(self, eng, ops, k, state, l_feet, v_ref, reduced=None, v_cur=None, h=None):
+    def plan(self, eng, ops, k, state, l_feet, v_ref, reduced=None, v_cur=None, h=None, params=None):
         return eng.plan(ops, k, state, l_feet, v_ref, self.gait, self.rot_flag, self.h_rot, self.xref,
-                        self.fsteps, reduced=reduced, v_cur=v_cur, h=h)
+                        self.fsteps, reduced=reduced, v_cur=v_cur, h=h, params=params)
 
 
 def _close(a, b, tol=PLAN_TOL):
@@ -53,7 +53,7 @@ def _close(a, b, tol=PLAN_TOL):
     return float(d.max(initial=0)), float((d == 0).mean())
 
 
-@pytest.mark.parametrize("N", [16, 32])
+@pytest.mark.parametrize("N", [8, 16, 24, 32])
 def test_planner_vs_reference_fixtures(mpcq, engines, N):
     """Every scenario of planner_golden.npz runs as one instance of a batch,
     tick by tick as processing.py:81-131 drives the reference."""
@@ -61,13 +61,15 @@ def test_planner_vs_reference_fixtures(mpcq, engines, N):
     eng = engines[N]
     S, T = G[f"n{N}_state"].shape[:2]
     bs = BatchState(G[f"n{N}_gait0"], N)
+    # the N = 8 / 24 fixtures ran FootstepPlanner(0.04, n_periods)
+    pp = mpcq.default_planner_params(dt=float(G[f"n{N}_dt"][0])) if f"n{N}_dt" in G.files else None
     worst, exact = 0.0, []
     for j in range(T):
         a = (G[f"n{N}_state"][:, j], G[f"n{N}_l_feet"][:, j], G[f"n{N}_v_ref"][:, j])
         red = G[f"n{N}_reduced"][:, j].astype(np.int32)
         if j == 0:
-            assert (bs.plan(eng, mpcq.PLAN_FOOTSTEPS, 0, *a, reduced=red) == 0).all()
-        assert (bs.plan(eng, mpcq.PLAN_TICK, j, *a, reduced=red) == 0).all()
+            assert (bs.plan(eng, mpcq.PLAN_FOOTSTEPS, 0, *a, reduced=red, params=pp) == 0).all()
+        assert (bs.plan(eng, mpcq.PLAN_TICK, j, *a, reduced=red, params=pp) == 0).all()
         assert np.array_equal(bs.gait, G[f"n{N}_gait"][:, j]), j
         assert np.array_equal(bs.rot_flag, G[f"n{N}_flag"][:, j]), j
         for got, want in ((bs.fsteps, G[f"n{N}_fsteps"][:, j]), (bs.xref, G[f"n{N}_xref"][:, j]),

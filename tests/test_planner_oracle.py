@@ -17,9 +17,14 @@ def gold():
     return np.load(GOLD)
 
 
+def _params(G, N):
+    # N = 8 / 24 fixtures run at dt = 0.04 (FootstepPlanner(0.04, n_periods)), the others at 0.02
+    return O.default_planner_params(dt=float(G[f"n{N}_dt"][0])) if f"n{N}_dt" in G.files else None
+
+
 def replay(G, N, s, check):
     """Drive one scenario through the oracle as processing.py:81-131 drives the reference."""
-    pl = O.Planner(N, G[f"n{N}_gait0"][s])
+    pl = O.Planner(N, G[f"n{N}_gait0"][s], params=_params(G, N))
     for j in range(G[f"n{N}_state"].shape[1]):
         a = dict(state=G[f"n{N}_state"][s, j], l_feet=G[f"n{N}_l_feet"][s, j],
                  v_ref=G[f"n{N}_v_ref"][s, j], reduced=bool(G[f"n{N}_reduced"][s, j]))
@@ -29,15 +34,25 @@ def replay(G, N, s, check):
         check(pl, j)
 
 
-@pytest.mark.parametrize("N", [16, 32])
+def _same(a, b, tol):
+    if tol == 0.0:
+        return np.array_equal(a, b, equal_nan=True)
+    return np.array_equal(np.isnan(a), np.isnan(b)) and np.nanmax(np.abs(a - b), initial=0.0) <= tol
+
+
+@pytest.mark.parametrize("N", [8, 16, 24, 32, 48])
 def test_planner_oracle_bit_exact(gold, N):
+    """Bit-identical at N <= 32.  At N = 48 numpy's vectorised sin / cos (arrays of 48
+    yaw values, angles up to ~1 rad) and the host libm differ by an ulp on a few
+    elements, so fsteps / xref there are held to 1e-15 (gait, flags still exact)."""
     G = gold
+    tol = 0.0 if N <= 32 else 1e-15
     for s in range(G[f"n{N}_state"].shape[0]):
         def check(pl, j):
             ctx = (N, str(G[f"n{N}_kind"][s]), j)
             assert np.array_equal(pl.gait, G[f"n{N}_gait"][s, j]), ctx
-            assert np.array_equal(pl.fsteps, G[f"n{N}_fsteps"][s, j], equal_nan=True), ctx
-            assert np.array_equal(pl.xref, G[f"n{N}_xref"][s, j]), ctx
+            assert _same(pl.fsteps, G[f"n{N}_fsteps"][s, j], tol), ctx
+            assert _same(pl.xref, G[f"n{N}_xref"][s, j], tol), ctx
             assert pl.flag[0] == G[f"n{N}_flag"][s, j], ctx
             assert pl.h_rot[0] == G[f"n{N}_h_rot"][s, j], ctx
         replay(G, N, s, check)
@@ -46,7 +61,7 @@ def test_planner_oracle_bit_exact(gold, N):
 def test_planner_oracle_fixture_coverage(gold):
     # the fixtures exercise every state of the rotation-command state machine
     # and both dx/dy branches (v_ref[5] == 0 and != 0)
-    for N in (16, 32):
+    for N in (8, 16, 24, 32, 48):
         assert set(np.unique(gold[f"n{N}_flag"]).tolist()) == {0, 1, 2}
         assert (gold[f"n{N}_v_ref"][..., 5] == 0).any() and (gold[f"n{N}_v_ref"][..., 5] != 0).any()
         assert gold[f"n{N}_reduced"].any()

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MPCQ_ABI_VERSION 1
+#define MPCQ_ABI_VERSION 2  /* 2: eps_prim_inf / eps_dual_inf, dual_warm, infeasibility statuses */
 
 /* error codes (return values) */
 #define MPCQ_OK 0
@@ -45,10 +45,16 @@ extern "C" {
 /* per-instance status (OSQP 0.6 status values, plus formulation errors) */
 #define MPCQ_STATUS_SOLVED 1
 #define MPCQ_STATUS_SOLVED_INACCURATE 2
+#define MPCQ_STATUS_PRIMAL_INFEASIBLE_INACCURATE 3
+#define MPCQ_STATUS_DUAL_INFEASIBLE_INACCURATE 4
 #define MPCQ_STATUS_MAX_ITER_REACHED (-2)
+#define MPCQ_STATUS_PRIMAL_INFEASIBLE (-3)  /* OSQP 0.6 is_primal_infeasible: x, y, f0 are NaN */
+#define MPCQ_STATUS_DUAL_INFEASIBLE (-4)    /* OSQP 0.6 is_dual_infeasible: x, y, f0 are NaN */
 #define MPCQ_STATUS_NONFINITE (-10)      /* NaN/Inf reached the solver */
 #define MPCQ_STATUS_BAD_GAIT (-11)       /* fsteps durations: no terminator / sum != N / NaN */
 #define MPCQ_STATUS_FACTOR_FAILED (-12)  /* KKT block lost positive definiteness */
+#define MPCQ_STATUS_BAD_BOUNDS (-13)     /* some l > u: osqp's setup / update reject the data
+                                            (the python wrapper raises ValueError); no solve */
 
 /* flags */
 #define MPCQ_FLAG_DEVICE_PTRS 1u  /* every array argument is a device pointer on ctx's device */
@@ -85,6 +91,8 @@ typedef struct mpcq_params {
   double eps_rel;           /* 1e-7 */
   double adaptive_rho_tolerance; /* 5 */
   double delta;             /* polish regularisation 1e-6 */
+  double eps_prim_inf;      /* 1e-4: primal infeasibility tolerance (OSQP 0.6 default) */
+  double eps_dual_inf;      /* 1e-4: dual infeasibility tolerance (OSQP 0.6 default) */
   int32_t max_iter;         /* 4000 */
   int32_t check_termination;/* 25 */
   int32_t adaptive_rho;     /* 1 */
@@ -95,7 +103,12 @@ typedef struct mpcq_params {
   int32_t polish_refine_iter; /* 3 */
   int32_t polish_rounds;    /* 1 = OSQP's single active-set guess; >1 iterates the
                                guess (primal-dual active set) until it repeats */
-  int32_t reserved[8];
+  int32_t dual_warm;        /* how warm_y / y are read and written (MPC.py:419-420):
+                               0: osqp's unscaled duals (warm_start(y=) in, results.y out);
+                               1: the solver's scaled workspace y, carried as is across the
+                                  re-scaled update(Ax=) + warm_start(x=) of the next tick --
+                                  what osqp 0.6 does between the reference's ticks */
+  int32_t reserved[7];
 } mpcq_params;
 
 typedef struct mpcq_ctx mpcq_ctx;

@@ -66,6 +66,9 @@ int check_params(const mpcq_params* p) {
   if (!(p->rho > 0) || !(p->sigma > 0) || !(p->alpha > 0 && p->alpha < 2))
     return fail(MPCQ_E_INVALID, "need rho > 0, sigma > 0, 0 < alpha < 2");
   if (!(p->eps_abs >= 0) || !(p->eps_rel >= 0)) return fail(MPCQ_E_INVALID, "eps must be >= 0");
+  if (!(p->eps_prim_inf >= 0) || !(p->eps_dual_inf >= 0))
+    return fail(MPCQ_E_INVALID, "eps_prim_inf / eps_dual_inf must be >= 0");
+  if (p->dual_warm != 0 && p->dual_warm != 1) return fail(MPCQ_E_INVALID, "dual_warm must be 0 or 1");
   if (p->max_iter < 1 || p->check_termination < 0 || p->scaling < 0 || p->adaptive_rho_interval < 0)
     return fail(MPCQ_E_INVALID, "max_iter >= 1, check_termination/scaling/interval >= 0");
   if (!(p->adaptive_rho_tolerance >= 1)) return fail(MPCQ_E_INVALID, "adaptive_rho_tolerance >= 1");
@@ -167,6 +170,8 @@ void mpcq_default_params(mpcq_params* p) {
   p->eps_rel = 1e-7;
   p->adaptive_rho_tolerance = 5.0;
   p->delta = 1e-6;
+  p->eps_prim_inf = 1e-4;
+  p->eps_dual_inf = 1e-4;
   p->max_iter = 4000;
   p->check_termination = 25;
   p->adaptive_rho = 1;
@@ -175,6 +180,7 @@ void mpcq_default_params(mpcq_params* p) {
   p->polish = 0;
   p->polish_refine_iter = 3;
   p->polish_rounds = 1;
+  p->dual_warm = 0;
 }
 
 int mpcq_dims(int N, int32_t* n, int32_t* m, int32_t* nnz) {

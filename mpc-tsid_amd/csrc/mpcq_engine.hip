@@ -29,6 +29,7 @@
 // stage lanes' registers.
 #include <math.h>
 
+#include <type_traits>
 #include <utility>
 
 #include "mpcq_internal.h"
@@ -622,6 +623,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       int bad = 0;
       for (int e = t; e < nnz; e += T)
         if (!isfinite(sh.Ab[e])) bad = 1;
+      int lgu = 0;  // l > u on an own row (osqp rejects the data)
       if constexpr (FUSED) {
         if (cl && isnan(bnd)) bad = 1;
       } else {
@@ -630,11 +632,12 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           if (isnan(lo_g[j]) || isnan(hi_g[j])) bad = 1;
           lo_g[j] = lo_g[j] < -kInf ? -kInf : lo_g[j];  // python osqp clamps to +-OSQP_INFTY
           hi_g[j] = hi_g[j] > kInf ? kInf : hi_g[j];
+          if (lo_g[j] > hi_g[j]) lgu = 1;
         }
       }
-      if (status == 0 && bad) atomicOr(&sh.flag[1], 1);
+      if (status == 0 && (bad || lgu)) atomicOr(&sh.flag[1], bad ? 1 : 2);
       sync_all();
-      if (status == 0 && sh.flag[1]) status = MPCQ_STATUS_NONFINITE;
+      if (status == 0 && sh.flag[1]) status = (sh.flag[1] & 1) ? MPCQ_STATUS_NONFINITE : MPCQ_STATUS_BAD_BOUNDS;
     }
 
     // persistent per-lane state (column values of c == 3 lanes are shadows)
@@ -1007,11 +1010,115 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       v = fmax(v, dppd<0x128>(v));
       return v;
     };
+    // A v on the own rows for own-column values (vf, vX), the previous stage's states in P
+    auto rowA = [&](double vf, double vX, lds_cd* P, double (&ax)[3]) __attribute__((always_inline)) {
+      double bco[12];
+#pragma unroll
+      for (int psi = 0; psi < 12; ++psi) {
+        const int fp = psi / 3, cp = psi % 3;
+        const double v = Ab[oB0 + 24 * fp + 7 * cp];
+        bco[psi] = (ph >= 9 || (isv && cp == ph - 6)) ? v : 0.0;
+      }
+      const double bfx = bdot_ln12(bco, vf, 0.0);
+      double dyn = Ab[oXd] * vX;
+      const double d1 = dyn + Ab[oHd] * P[oXSp - 12];
+      const double d2 = d1 + Ab[oH6] * P[oXSp6 - 12];
+      dyn = hp ? (isv ? d1 : d2) : dyn;
+      dyn = isv ? dyn + bfx : dyn;
+      const double q0 = qbc<0>(vf), q1 = qbc<1>(vf), q2 = qbc<2>(vf);
+      const double frA = Ab[oFb] * q2 + Ab[oFa] * (ta0 ? q0 : q1);
+      const double frB = Ab[oF4] * q2;
+      const double swg = Ab[oF + 4] * vf;
+      ax[0] = cl ? dyn : frA;
+      ax[1] = cl ? swg : frB;
+      ax[2] = cl ? frA : 0.0;
+    };
+    // A' w on the own columns for own-row values w, the next stage's dynamics-row w in W
+    auto colAt = [&](const double (&w)[3], const double* W, double& atf, double& atX)
+        __attribute__((always_inline)) {
+      atf = colF_off(w);
+      const double* wn = W + 12 * (k < N - 1 ? k + 1 : k);
+      const double sXv = Ab[oXd] * w[0];
+      const double x1 = sXv + Ab[oXd + 1] * wn[isv ? ph - 6 : ph];
+      const double x2 = x1 + Ab[oXd + 2] * wn[ph];
+      atX = k < N - 1 ? (isv ? x2 : x1) : sXv;
+    };
+    // OSQP 0.6's infeasibility tests (auxil.c is_primal_infeasible / is_dual_infeasible)
+    // on the last iteration's delta_y (dy, own rows) and delta_x (dxf, dxX, own
+    // columns), in a pass of their own right after the update, while the deltas are
+    // live: the deltas of the states / dynamics-row duals go through na / nb (free
+    // between the sweeps); the per-wave partials land in red[32 wv + 16 ..] and are
+    // combined by update_info(INF) after its barrier, which also turns them into the
+    // uniform flags (each test only where its residual test fails, as osqp's
+    // check_termination).
+    // outcome bits (one uniform int: the loop carries it): 1 primal, 2 dual infeasible
+    // at the check's tolerances, 4 / 8 at the approximate (x10) ones
+    int inf_bits = 0;
+    auto infeas_pass = [&](const double (&dy)[3], double dxf, double dxX) __attribute__((always_inline)) {
+      double dyp[3];  // delta_y projected onto the polar of the recession cone of [l, u]
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const bool uinf = hi_of(j) > kInf * kMinScaling, linf = lo_of(j) < -kInf * kMinScaling;
+        dyp[j] = uinf ? (linf ? 0.0 : fmin(dy[j], 0.0)) : (linf ? fmax(dy[j], 0.0) : dy[j]);
+      }
+      if (cl) { sh.u.it.na[k][ph] = dxX; sh.u.it.nb[k][ph] = dyp[0]; }
+      sync_all();
+      launder_p();
+      double ndy = 0.0, vu = -INFINITY, vl = -INFINITY, ineq = 0.0;
+      {
+        double adx[3];
+        rowA(dxf, dxX, (lds_cd*)&sh.u.it.na[0][0], adx);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const double lj = lo_of(j), hj = hi_of(j), v = adx[j] / E[j];
+          ndy = fmax(ndy, fabs(E[j] * dyp[j]));
+          ineq += hj * fmax(dyp[j], 0.0) + lj * fmin(dyp[j], 0.0);
+          if (hj < kInf * kMinScaling) vu = fmax(vu, v);
+          if (lj > -kInf * kMinScaling) vl = fmax(vl, -v);
+        }
+      }
+      double q3[3] = {0.0, 0.0, 0.0};
+      {
+        double dtf, dtX;
+        colAt(dyp, &sh.u.it.nb[0][0], dtf, dtX);
+        if (cl) {
+          const double dif = 1.0 / Df, diX = 1.0 / DX;
+          q3[0] = fmax(fabs(dtf * dif), fabs(dtX * diX));                  // ||D^-1 A' dy||
+          q3[1] = fmax(fabs(Df * dxf), fabs(DX * dxX));                    // ||D dx||
+          q3[2] = fmax(fabs(Pbf() * dxf * dif), fabs(PbX() * dxX * diX));  // ||D^-1 P dx||
+        }
+      }
+      // maxima over the wave (lanes 0..5 keep quantity s), the sum by xor butterflies
+      double mx[6] = {ndy, q3[0], q3[1], q3[2], vu, vl}, mine = 0.0;
+#pragma unroll
+      for (int e = 0; e < 6; ++e) {
+        const double v = row_max(mx[e]);
+        mine = s == e ? v : mine;
+      }
+      mine = pair_max(row_pair_max(mine));
+      ineq += dppd<0xB1>(ineq);
+      ineq += dppd<0x4E>(ineq);
+      ineq += dppd<0x124>(ineq);
+      ineq += dppd<0x128>(ineq);
+      ineq = row_pair_sum(ineq);
+      {
+        const long long bb = __double_as_longlong(ineq);
+        const auto lo_ = __builtin_amdgcn_permlane32_swap((unsigned)bb, (unsigned)bb, false, false);
+        const auto hi_ = __builtin_amdgcn_permlane32_swap((unsigned)(bb >> 32), (unsigned)(bb >> 32), false, false);
+        ineq = __longlong_as_double(((long long)hi_[0] << 32) | lo_[0]) +
+               __longlong_as_double(((long long)hi_[1] << 32) | lo_[1]);
+      }
+      if (lane < 6) sh.red[32 * wv + 16 + lane] = mine;
+      if (lane == 6) sh.red[32 * wv + 16 + 6] = ineq;
+      // (update_info's first barrier publishes these)
+    };
     // The states and dynamics-row duals are published in yv / bo, which the sweeps
     // no longer need (xs still feeds the force recovery of slower waves); lane s
     // of each row then owns residual quantity s, reduced over the wave's rows by
-    // permlane swaps and over the waves through red[].
-    auto update_info = [&]() __attribute__((always_inline)) {
+    // permlane swaps and over the waves through red[].  INF: also combine the
+    // partials of infeas_pass.
+    auto update_info = [&](auto inf_tag) __attribute__((always_inline)) {
+      constexpr bool INF = decltype(inf_tag)::value;
       if (cl) { sh.u.it.yv[k][ph] = xX; sh.u.it.bo[k][ph] = y[0]; }
       sync_all();
       STAMP(4);
@@ -1020,28 +1127,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       double mine = 0.0;                              // this lane's row maximum (quantity s)
       {  // primal side: A x - z on the own rows
         double ax[3], q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        {
-          double bco[12];
-#pragma unroll
-          for (int psi = 0; psi < 12; ++psi) {
-            const int fp = psi / 3, cp = psi % 3;
-            const double v = Ab[oB0 + 24 * fp + 7 * cp];
-            bco[psi] = (ph >= 9 || (isv && cp == ph - 6)) ? v : 0.0;
-          }
-          const double bfx = bdot_ln12(bco, xf, 0.0);
-          double dyn = Ab[oXd] * xX;
-          const double d1 = dyn + Ab[oHd] * YV[oXSp - 12];
-          const double d2 = d1 + Ab[oH6] * YV[oXSp6 - 12];
-          dyn = hp ? (isv ? d1 : d2) : dyn;
-          dyn = isv ? dyn + bfx : dyn;
-          const double q0 = qbc<0>(xf), q1 = qbc<1>(xf), q2 = qbc<2>(xf);
-          const double frA = Ab[oFb] * q2 + Ab[oFa] * (ta0 ? q0 : q1);
-          const double frB = Ab[oF4] * q2;
-          const double swg = Ab[oF + 4] * xf;
-          ax[0] = cl ? dyn : frA;
-          ax[1] = cl ? swg : frB;
-          ax[2] = cl ? frA : 0.0;
-        }
+        rowA(xf, xX, YV, ax);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           const double ei = 1.0 / E[j], d = ax[j] - z[j];
@@ -1061,15 +1147,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       STAMP(5);
       {  // dual side: P x + A' y on the own columns
         double q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        const double atf = colF_off(y);
-        double atX;
-        {
-          const double* yn = sh.u.it.bo[k < N - 1 ? k + 1 : k];  // next stage's dynamics-row y
-          const double sXv = Ab[oXd] * y[0];
-          const double x1 = sXv + Ab[oXd + 1] * yn[isv ? ph - 6 : ph];
-          const double x2 = x1 + Ab[oXd + 2] * yn[ph];
-          atX = k < N - 1 ? (isv ? x2 : x1) : sXv;
-        }
+        double atf, atX;
+        colAt(y, &sh.u.it.bo[0][0], atf, atX);
         const double pxf = Pbf() * xf, pxX = PbX() * xX;
         const double dif = 1.0 / Df, diX = 1.0 / DX;
         const double df_ = pxf + atf, dX_ = pxX + atX;
@@ -1088,7 +1167,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         }
       }
       mine = pair_max(row_pair_max(mine));  // the wave's four rows
-      if (lane < 12) sh.red[12 * wv + lane] = mine;
+      if (lane < 12) sh.red[32 * wv + lane] = mine;
       sync_all();
       STAMP(8);
       double qv[12];
@@ -1096,7 +1175,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         const int e = s < 12 ? s : 0;
         double v = sh.red[e];
 #pragma unroll
-        for (int w = 1; w < NW; ++w) v = fmax(v, sh.red[12 * w + e]);
+        for (int w = 1; w < NW; ++w) v = fmax(v, sh.red[32 * w + e]);
         gather_direct12(v, qv);
       }
       const double cinv = 1.0 / cscale;
@@ -1109,6 +1188,32 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       // uniform by construction; readfirstlane lets the compiler see it
       pri_res = uni(pri_res); dua_res = uni(dua_res); eps_pri = uni(eps_pri);
       eps_dua = uni(eps_dua); s_pri = uni(s_pri); s_dua = uni(s_dua);
+
+      if constexpr (INF) {
+        const int e = s < 7 ? s : 0;
+        double v = sh.red[16 + e];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) {
+          const double t2 = sh.red[32 * w + 16 + e];
+          v = s == 6 ? v + t2 : fmax(v, t2);
+        }
+        // kept in VGPRs (every lane holds the same values) and folded into one uniform
+        // int at the end: SGPRs here would push loop-carried scalars into VGPR lanes
+        // (v_readlane on the hot path, measured)
+        const double ndy = rbc<0>(v), naty = rbc<1>(v), ndx = rbc<2>(v), npdx = rbc<3>(v);
+        const double vu = rbc<4>(v), vl = rbc<5>(v), ineq = rbc<6>(v);
+        int bits = 0;
+#pragma unroll
+        for (int fi = 0; fi < 2; ++fi) {
+          const double f = fi == 0 ? 1.0 : 10.0, epi = f * p.eps_prim_inf, edi = f * p.eps_dual_inf;
+          const bool pi = !(pri_res < f * eps_pri) && ndy > kDivTol && ineq < epi * ndy && naty < epi * ndy;
+          const bool di = !(dua_res < f * eps_dua) && ndx > kDivTol && 0.0 < cscale * edi * ndx &&
+                          npdx < cscale * edi * ndx && !(vu > edi * ndx) && !(vl > edi * ndx);
+          bits |= (pi ? 1 : 0) << (2 * fi);
+          bits |= (di ? 2 : 0) << (2 * fi);
+        }
+        inf_bits = __builtin_amdgcn_readfirstlane(bits);
+      }
       sync_all();
     };
     auto converged = [&](double fac) __attribute__((always_inline)) {
@@ -1247,7 +1352,10 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           const int r = nat_row(j);
-          y[j] = r >= 0 ? cscale * a.warm_y[b * m + r] / E[j] : 0.0;
+          // dual_warm = 1: osqp's workspace y from the previous solve, kept as is across the
+          // re-scaled update(Ax=) (MPC.py:419-420); 0: osqp_warm_start_y's scaling
+          const double wy = r >= 0 ? a.warm_y[b * m + r] : 0.0;
+          y[j] = r >= 0 ? (p.dual_warm ? wy : cscale * wy / E[j]) : 0.0;
         }
       }
       sync_all();
@@ -1489,9 +1597,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       bool last_checked = false;
       int iter = 1;
       int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
-      double lo[3], hi[3];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) { lo[j] = lo_of(j); hi[j] = hi_of(j); }
+      // the bounds are re-derived where used (lo_of / hi_of: a select on the lane's
+      // class and its row scaling in the fused path) rather than held in 6 registers
       for (;;) {
 #ifndef MPCQ_REP_FACTOR
 #define MPCQ_REP_FACTOR 1
@@ -1508,61 +1615,93 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         if (!fac_ok) { status = MPCQ_STATUS_FACTOR_FAILED; break; }
         STAMP(2);
         bool refactor = false;
-        for (; iter <= p.max_iter; ++iter) {
+        // One ADMM iteration (osqp update_xz_tilde / update_x / update_z / update_y).
+        // DELTA: also keep delta_y / delta_x (the last iteration before a check, for the
+        // infeasibility tests).  The iterations between two checks run in a loop of
+        // their own without them, so the check / infeasibility code and its live values
+        // sit outside the hot loop's register allocation (inside it, they cost 0.31 us
+        // per iteration through spills on the sweep path, measured).
+        auto admm_iter = [&](auto delta_tag, double (&dyv)[3], double& dxf_, double& dxX_)
+            __attribute__((always_inline)) {
+          constexpr bool DELTA = decltype(delta_tag)::value;
           double uf, beta, sf, sX, ax[3];
           ph_rhs(true, kNoW, 0.0, 0.0, uf, beta);
           ph_sweep();
           ph_recover(uf, beta, sf, sX, ax);
-          // P9: z, y update (osqp update_z / update_y), x update
-          {
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-              const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
-              const double tt = zr + ri[j] * y[j];
-              const double zn = fmin(fmax(tt, lo[j]), hi[j]);  // osqp project: c_min(c_max(tt, l), u)
-              y[j] = y[j] + rr[j] * (zr - zn);
-              z[j] = zn;
-            }
-            xf = p.alpha * sf + (1.0 - p.alpha) * xf;
-            xX = p.alpha * sX + (1.0 - p.alpha) * xX;
+          for (int j = 0; j < 3; ++j) {
+            const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
+            const double tt = zr + ri[j] * y[j];
+            const double zn = fmin(fmax(tt, lo_of(j)), hi_of(j));  // osqp project: c_min(c_max(tt, l), u)
+            const double d = rr[j] * (zr - zn);
+            if constexpr (DELTA) dyv[j] = d;
+            y[j] = y[j] + d;
+            z[j] = zn;
           }
+          const double nxf = p.alpha * sf + (1.0 - p.alpha) * xf;
+          const double nxX = p.alpha * sX + (1.0 - p.alpha) * xX;
+          if constexpr (DELTA) { dxf_ = nxf - xf; dxX_ = nxX - xX; }
+          xf = nxf;
+          xX = nxX;
           STAMP(10);
+        };
+        const bool chk_on = p.check_termination > 0;
+        const bool adp_on = p.adaptive_rho && p.adaptive_rho_interval > 0;
+        while (iter <= p.max_iter) {
+          // the next event: a termination check, an adaptive-rho step or the last iteration
+          int until = p.max_iter - iter + 1;
+          if (chk_on && to_check < until) until = to_check;
+          if (adp_on && to_adapt < until) until = to_adapt;
+          double dyv[3], dxf_, dxX_;
+#pragma nounroll
+          for (int r_ = 1; r_ < until; ++r_, ++iter) admm_iter(std::false_type{}, dyv, dxf_, dxX_);
+          admm_iter(std::true_type{}, dyv, dxf_, dxX_);
           // iter % check_termination == 0 / iter % adaptive_rho_interval == 0, by countdown
-          const bool can_check = p.check_termination > 0 && --to_check == 0;
+          const bool can_check = chk_on && (to_check -= until) == 0;
           if (can_check) to_check = p.check_termination;
-          const bool adapt = p.adaptive_rho && p.adaptive_rho_interval > 0 && --to_adapt == 0;
+          const bool adapt = adp_on && (to_adapt -= until) == 0;
           if (adapt) to_adapt = p.adaptive_rho_interval;
           last_checked = can_check;
-          if (can_check || adapt) {
-            update_info();
-            if (!(isfinite(pri_res) && isfinite(dua_res))) { status = MPCQ_STATUS_NONFINITE; break; }
-            if (can_check && converged(1.0)) { status = MPCQ_STATUS_SOLVED; break; }
-            if (adapt) {
-              double rn = rho_s * sqrt(s_pri / (s_dua + kDivTol));
-              rn = fmin(fmax(rn, kRhoMin), kRhoMax);
-              if (rn > rho_s * p.adaptive_rho_tolerance || rn < rho_s / p.adaptive_rho_tolerance) {
-                rho_s = rn;
-                set_rho();
-                refactor = true;
-                ++n_upd;
-                ++iter;
-                sync_all();
-                break;
-              }
+          // the last iteration's information is always formed here, while its deltas are
+          // live (osqp's update_info after the loop when the last iteration was unchecked)
+          infeas_pass(dyv, dxf_, dxX_);
+          update_info(std::true_type{});
+          if (!(isfinite(pri_res) && isfinite(dua_res))) { status = MPCQ_STATUS_NONFINITE; break; }
+          if (can_check) {  // osqp check_termination
+            if (converged(1.0)) { status = MPCQ_STATUS_SOLVED; break; }
+            if (inf_bits & 1) { status = MPCQ_STATUS_PRIMAL_INFEASIBLE; break; }
+            if (inf_bits & 2) { status = MPCQ_STATUS_DUAL_INFEASIBLE; break; }
+          }
+          if (adapt) {
+            double rn = rho_s * sqrt(s_pri / (s_dua + kDivTol));
+            rn = fmin(fmax(rn, kRhoMin), kRhoMax);
+            if (rn > rho_s * p.adaptive_rho_tolerance || rn < rho_s / p.adaptive_rho_tolerance) {
+              rho_s = rn;
+              set_rho();
+              refactor = true;
+              ++n_upd;
+              ++iter;
+              sync_all();
+              break;
             }
           }
           STAMP(11);
+          ++iter;
         }
         if (!refactor) break;
       }
       it_done = iter > p.max_iter ? p.max_iter : iter;
       if (status == 0) {
-        if (!last_checked) {
-          update_info();
+        if (!last_checked) {  // the information of the last (unchecked) iteration
           if (converged(1.0)) status = MPCQ_STATUS_SOLVED;
+          else if (inf_bits & 1) status = MPCQ_STATUS_PRIMAL_INFEASIBLE;
+          else if (inf_bits & 2) status = MPCQ_STATUS_DUAL_INFEASIBLE;
         }
-        if (status == 0)
-          status = converged(10.0) ? MPCQ_STATUS_SOLVED_INACCURATE : MPCQ_STATUS_MAX_ITER_REACHED;
+        if (status == 0)  // the approximate check (tolerances x10)
+          status = converged(10.0) ? MPCQ_STATUS_SOLVED_INACCURATE
+                   : (inf_bits & 4) ? MPCQ_STATUS_PRIMAL_INFEASIBLE_INACCURATE
+                   : (inf_bits & 8) ? MPCQ_STATUS_DUAL_INFEASIBLE_INACCURATE
+                                   : MPCQ_STATUS_MAX_ITER_REACHED;
       }
 
       // ------------------------------------------------------------ polish
@@ -1604,21 +1743,21 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               int a_ = 0;
               if (r >= 0) {
                 if (rd == 0) {  // OSQP's guess (polish.c form_Ared)
-                  if (zs[j] - lo[j] < -ys[j]) a_ = -1;
-                  else if (hi[j] - zs[j] < ys[j]) a_ = 1;
+                  if (zs[j] - lo_of(j) < -ys[j]) a_ = -1;
+                  else if (hi_of(j) - zs[j] < ys[j]) a_ = 1;
                   if (eq && a_ == 0) a_ = 1;
                 } else {  // keep correctly signed active rows, add violated rows
                   const double tol = 1e-12;
                   if (prv[j] == -1 && (ys[j] <= tol || eq)) a_ = -1;
                   else if (prv[j] == 1 && (ys[j] >= -tol || eq)) a_ = 1;
-                  else if (zs[j] < lo[j] - tol) a_ = -1;
-                  else if (zs[j] > hi[j] + tol) a_ = 1;
+                  else if (zs[j] < lo_of(j) - tol) a_ = -1;
+                  else if (zs[j] > hi_of(j) + tol) a_ = 1;
                 }
               }
               changed |= a_ != prv[j];
               act[j] = a_;
               prv[j] = a_;
-              bred[j] = a_ < 0 ? lo[j] : (a_ > 0 ? hi[j] : 0.0);
+              bred[j] = a_ < 0 ? lo_of(j) : (a_ > 0 ? hi_of(j) : 0.0);
               prho[j] = a_ ? kPolishRho : 0.0;
             }
             if (rd > 0) {  // stop when the set repeats (uniform over the block)
@@ -1691,7 +1830,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
               const double tt = axp[j] + yp[j];
-              const double zz = fmin(fmax(tt, lo[j]), hi[j]);
+              const double zz = fmin(fmax(tt, lo_of(j)), hi_of(j));
               z[j] = zz;
               y[j] = tt - zz;
             }
@@ -1700,9 +1839,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               for (int j = 0; j < 3; ++j)
                 if (fabs(y[j] - yp[j]) > 1e-9 || (act[j] == 0 && fabs(axp[j] - z[j]) > 1e-12))
                   printf("blk0 k %d s %d j %d row %d act %d bred %.3e ax %.6e yp %.3e -> z %.6e y %.3e lo %.3e hi %.3e\n",
-                         k, s, j, nat_row(j), act[j], bred[j], axp[j], yp[j], z[j], y[j], lo[j], hi[j]);
+                         k, s, j, nat_row(j), act[j], bred[j], axp[j], yp[j], z[j], y[j], lo_of(j), hi_of(j));
 #endif
-            update_info();
+            update_info(std::false_type{});
 #ifdef MPCQ_DEBUG_POLISH
             if (b < 2 && t == 0) printf("blk %d rd %d admm pri %.3e dua %.3e | polished pri %.3e dua %.3e eps %.3e %.3e\n", (int)b, rd, a_pri, a_dua, pri_res, dua_res, eps_pri, eps_dua);
 #endif
@@ -1734,8 +1873,12 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       }
     }
     // ------------------------------------------------------------ outputs
+    // osqp store_solution: no solution (x = y = NaN) for the infeasibility statuses
     const bool nan_out = status == MPCQ_STATUS_NONFINITE || status == MPCQ_STATUS_FACTOR_FAILED ||
-                         status == MPCQ_STATUS_BAD_GAIT;
+                         status == MPCQ_STATUS_BAD_GAIT || status == MPCQ_STATUS_BAD_BOUNDS ||
+                         status == MPCQ_STATUS_PRIMAL_INFEASIBLE ||
+                         status == MPCQ_STATUS_DUAL_INFEASIBLE || status == MPCQ_STATUS_PRIMAL_INFEASIBLE_INACCURATE ||
+                         status == MPCQ_STATUS_DUAL_INFEASIBLE_INACCURATE;
     if (cl) {
       const double vf = nan_out ? NAN : Df * xf, vX = nan_out ? NAN : DX * xX;
       if (a.x) { a.x[b * n + colF] = vf; a.x[b * n + colX] = vX; }
@@ -1745,7 +1888,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int r = nat_row(j);
-        if (r >= 0) a.y[b * m + r] = nan_out ? NAN : E[j] * y[j] / cscale;
+        // dual_warm = 1: the scaled workspace y, what the next tick's warm start reads
+        if (r >= 0) a.y[b * m + r] = nan_out ? NAN : (p.dual_warm ? y[j] : E[j] * y[j] / cscale);
       }
     }
 #ifdef MPCQ_STAMPS

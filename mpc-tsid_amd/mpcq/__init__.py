@@ -15,7 +15,9 @@ from ._lib import (FLAG_ASYNC, FLAG_DEVICE_PTRS, MODE_SETUP, MODE_UPDATE,  # noq
                    default_planner_params, STATUS_BAD_GAIT, SV_COST, SV_F0, SV_FSTEPS, SV_GAIT,
                    SV_H_ROT, SV_ITERS, SV_L_FEET, SV_Q_W, SV_RHO, SV_ROT_FLAG, SV_STATE, SV_STATUS, SV_X,
                    SV_X_ROBOT, SV_XREF, SV_Y, STATUS_FACTOR_FAILED, STATUS_MAX_ITER_REACHED,
-                   STATUS_NONFINITE, STATUS_SOLVED, STATUS_SOLVED_INACCURATE, MpcqError,
+                   STATUS_NONFINITE, STATUS_SOLVED, STATUS_SOLVED_INACCURATE, STATUS_PRIMAL_INFEASIBLE,
+                   STATUS_DUAL_INFEASIBLE, STATUS_PRIMAL_INFEASIBLE_INACCURATE,
+                   STATUS_DUAL_INFEASIBLE_INACCURATE, STATUS_BAD_BOUNDS, MpcqError,
                    Params, build, default_params, lib, supported_horizons)
 from .engine import Engine, dims, pattern  # noqa: F401
 from .session import Session  # noqa: F401

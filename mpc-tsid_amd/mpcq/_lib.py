@@ -20,13 +20,20 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# MPCQ_LIB_VARIANT=stamps loads the diagnostic build of the same Makefile
-# (per-phase cycle stamps, tools/stamps.py); no other variant exists
-_VARIANT = os.environ.get("MPCQ_LIB_VARIANT")
-if _VARIANT not in (None, "", "stamps"):
-    raise ImportError(f"MPCQ_LIB_VARIANT={_VARIANT!r}: only 'stamps' (the diagnostic build) exists")
-LIB_PATH = os.path.join(HERE, "libmpcq_stamps.so" if _VARIANT else "libmpcq.so")
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+# MPCQ_LIB_VARIANT=stamps loads the diagnostic build of the same Makefile
+# (per-phase cycle stamps, tools/stamps.py); MPCQ_LIB_VARIANT=exp:<name> loads an
+# experiment build from csrc/build/variants (tools/build_variant.sh, timing tools
+# only -- outside the package, never shipped)
+_VARIANT = os.environ.get("MPCQ_LIB_VARIANT") or ""
+if _VARIANT == "stamps":
+    LIB_PATH = os.path.join(HERE, "libmpcq_stamps.so")
+elif _VARIANT.startswith("exp:"):
+    LIB_PATH = os.path.join(CSRC, "build", "variants", f"libmpcq_{_VARIANT[4:]}.so")
+elif _VARIANT:
+    raise ImportError(f"MPCQ_LIB_VARIANT={_VARIANT!r}: 'stamps' or 'exp:<name>'")
+else:
+    LIB_PATH = os.path.join(HERE, "libmpcq.so")
 
 # return codes / status / flags / modes (include/mpcq.h)
 OK = 0
@@ -34,9 +41,14 @@ E_INVALID, E_DEVICE, E_NOMEM, E_UNSUPPORTED = -1, -2, -3, -4
 STATUS_SOLVED = 1
 STATUS_SOLVED_INACCURATE = 2
 STATUS_MAX_ITER_REACHED = -2
+STATUS_PRIMAL_INFEASIBLE = -3
+STATUS_DUAL_INFEASIBLE = -4
+STATUS_PRIMAL_INFEASIBLE_INACCURATE = 3
+STATUS_DUAL_INFEASIBLE_INACCURATE = 4
 STATUS_NONFINITE = -10
 STATUS_BAD_GAIT = -11
 STATUS_FACTOR_FAILED = -12
+STATUS_BAD_BOUNDS = -13
 FLAG_DEVICE_PTRS = 1
 FLAG_ASYNC = 2
 MODE_UPDATE = 0
@@ -81,6 +93,8 @@ class Params(C.Structure):
         ("eps_rel", C.c_double),
         ("adaptive_rho_tolerance", C.c_double),
         ("delta", C.c_double),
+        ("eps_prim_inf", C.c_double),
+        ("eps_dual_inf", C.c_double),
         ("max_iter", C.c_int32),
         ("check_termination", C.c_int32),
         ("adaptive_rho", C.c_int32),
@@ -89,7 +103,8 @@ class Params(C.Structure):
         ("polish", C.c_int32),
         ("polish_refine_iter", C.c_int32),
         ("polish_rounds", C.c_int32),
-        ("reserved", C.c_int32 * 8),
+        ("dual_warm", C.c_int32),
+        ("reserved", C.c_int32 * 7),
     ]
 
     def as_dict(self):

@@ -18,10 +18,12 @@ The tick path is formulate (MPC.update_ML / update_NK, or create_* at k == 0)
 then the OSQP-0.6 solve with the reference's warm start (MPC.py:403-406): x is
 the previous solution shifted by one stage (states: last stage zeroed; forces:
 wrapped, as np.roll does), y and rho carry over from the previous solve as the
-osqp workspace does.  One difference is documented rather than hidden: osqp
-keeps y in its *scaled* coordinates across ``update(Ax=...)`` (which recomputes
-the Ruiz scaling), while the engine carries the unscaled dual and rescales it
-with the new scaling; the two agree whenever the scaling is unchanged.
+osqp workspace does.  The dual is carried the way osqp 0.6 carries it
+(params.dual_warm = 1, the façade's default): ``update(Ax=...)`` recomputes the
+Ruiz scaling but leaves the workspace y in the previous tick's *scaled*
+coordinates, and ``warm_start(x=...)`` (MPC.py:419-420) does not touch it; the
+engine then reads and returns that scaled y as is.  ``dual_warm=0`` carries the
+unscaled dual instead (osqp's explicit ``warm_start(y=...)``).
 
 Errors: the reference crashes on a gait table without a zero-duration
 terminator (MPC.py:636 ``next(...)[0]``) or whose durations do not sum to N
@@ -47,6 +49,7 @@ class MPC:
         self.dt = float(dt)
         self.n_steps = int(n_steps)
         self.T_gait = T_gait
+        overrides.setdefault("dual_warm", 1)  # osqp's workspace-y carry-over (MPC.py:419-420)
         self.engine = engine if engine is not None else Engine(self.n_steps, device=device, dt=self.dt, **overrides)
         p = self.engine.params
         self.mass = p.mass

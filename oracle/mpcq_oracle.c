@@ -19,9 +19,16 @@
  *     sigma 1e-6, alpha 1.6, termination check every 25 iterations with
  *     unscaled residuals, adaptive rho (interval = 4 x check_termination, the
  *     library's non-timed rule), max_iter 4000, optional polish (delta 1e-6,
- *     3 refinement steps).  Infeasibility detection is not restated (every
- *     MPC instance is feasible: f = 0 with the dynamics roll-out satisfies all
- *     rows).  The linear system is the reduced KKT P + sigma I + A' R A,
+ *     3 refinement steps), OSQP 0.6's infeasibility detection
+ *     (auxil.c is_primal_infeasible / is_dual_infeasible on the last iteration's
+ *     delta_y / delta_x at every termination check, eps_prim_inf = eps_dual_inf
+ *     = 1e-4; statuses -3 / -4, and 3 / 4 from the approximate check at
+ *     max_iter; x and y NaN then, as osqp's store_solution) -- every instance
+ *     MPC.py builds is feasible (f = 0 with the dynamics roll-out satisfies all
+ *     rows), so only hand-made data reach them.  params.dual_warm = 1 reads and
+ *     writes y in the solver's scaled coordinates, the workspace y osqp carries
+ *     across the reference's update(Ax=) + warm_start(x=) (MPC.py:419-420).
+ *     The linear system is the reduced KKT P + sigma I + A' R A,
  *     factored as a block-tridiagonal Cholesky over stages z_k = [f_k; X_k+1]
  *     (exact, like OSQP's QDLDL on the quasi-definite form).
  */
@@ -71,6 +78,8 @@ void oracle_default_params(mpcq_params* p) {
   p->eps_rel = 1e-7;
   p->adaptive_rho_tolerance = 5.0;
   p->delta = 1e-6;
+  p->eps_prim_inf = 1e-4;
+  p->eps_dual_inf = 1e-4;
   p->max_iter = 4000;
   p->check_termination = 25;
   p->adaptive_rho = 1;
@@ -79,6 +88,7 @@ void oracle_default_params(mpcq_params* p) {
   p->polish = 0;
   p->polish_refine_iter = 3;
   p->polish_rounds = 1;
+  p->dual_warm = 0;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -269,6 +279,7 @@ typedef struct {
   double *Kd, *Ko;
   /* ADMM vectors */
   double *x, *z, *y, *xt, *zt, *xp, *zp, *rhs, *w, *Ax, *Px, *Aty, *tmpn, *tmpm;
+  double *dy, *dx, *tmpm2, *tmpn2;  /* delta_y, delta_x of the last iteration (osqp update_y / update_x) */
   int *ctype;
 } Work;
 
@@ -278,7 +289,7 @@ static void work_free(Work* W) {
   void* ptrs[] = {W->colptr, W->rowidx, W->rowptr, W->colidx, W->cscpos, W->stage, W->loc,
                   W->Pd, W->A, W->lo, W->hi, W->D, W->E, W->rho, W->Kd, W->Ko,
                   W->x, W->z, W->y, W->xt, W->zt, W->xp, W->zp, W->rhs, W->w, W->Ax,
-                  W->Px, W->Aty, W->tmpn, W->tmpm, W->ctype};
+                  W->Px, W->Aty, W->tmpn, W->tmpm, W->ctype, W->dy, W->dx, W->tmpm2, W->tmpn2};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
 }
 
@@ -297,10 +308,10 @@ static int work_init(Work* W, int N) {
   W->Pd = xalloc(8 * n); W->A = xalloc(8 * nnz); W->lo = xalloc(8 * m); W->hi = xalloc(8 * m);
   W->D = xalloc(8 * n); W->E = xalloc(8 * m); W->rho = xalloc(8 * m);
   W->Kd = xalloc(8 * (size_t)N * 576); W->Ko = xalloc(8 * (size_t)N * 576);
-  double** vn[] = {&W->x, &W->xt, &W->xp, &W->rhs, &W->Px, &W->Aty, &W->tmpn};
-  for (size_t i = 0; i < 7; ++i) *vn[i] = xalloc(8 * n);
-  double** vm[] = {&W->z, &W->y, &W->zt, &W->zp, &W->w, &W->Ax, &W->tmpm};
-  for (size_t i = 0; i < 7; ++i) *vm[i] = xalloc(8 * m);
+  double** vn[] = {&W->x, &W->xt, &W->xp, &W->rhs, &W->Px, &W->Aty, &W->tmpn, &W->dx, &W->tmpn2};
+  for (size_t i = 0; i < 9; ++i) *vn[i] = xalloc(8 * n);
+  double** vm[] = {&W->z, &W->y, &W->zt, &W->zp, &W->w, &W->Ax, &W->tmpm, &W->dy, &W->tmpm2};
+  for (size_t i = 0; i < 9; ++i) *vm[i] = xalloc(8 * m);
   W->ctype = xalloc(sizeof(int) * m);
   if (!W->ctype || !W->tmpm) return -1;
   oracle_pattern(N, W->colptr, W->rowidx);
@@ -565,6 +576,73 @@ static int check_term(const Info* I, const mpcq_params* p, int approximate) {
   return (I->pri_res < eps_pri) && (I->dua_res < eps_dua);
 }
 
+/* osqp 0.6 auxil.c is_primal_infeasible, on the scaled data and the last
+ * iteration's delta_y: project delta_y onto the polar of the recession cone of
+ * [l, u], then ||E dy|| > 0, u'max(dy, 0) + l'min(dy, 0) < eps ||E dy|| and
+ * ||D^-1 A' dy|| < eps ||E dy||. */
+static int is_primal_infeasible(Work* W, double eps) {
+  const int m = W->m, n = W->n;
+  double* dy = W->dy;
+  for (int r = 0; r < m; ++r) {
+    if (W->hi[r] > OSQP_INFTY * MIN_SCALING) {
+      if (W->lo[r] < -OSQP_INFTY * MIN_SCALING) dy[r] = 0.0;
+      else dy[r] = dy[r] < 0.0 ? dy[r] : 0.0;
+    } else if (W->lo[r] < -OSQP_INFTY * MIN_SCALING) {
+      dy[r] = dy[r] > 0.0 ? dy[r] : 0.0;
+    }
+  }
+  double norm = 0.0;
+  for (int r = 0; r < m; ++r) { double a = fabs(W->E[r] * dy[r]); if (a > norm) norm = a; }
+  if (!(norm > DIV_TOL)) return 0;
+  double ineq = 0.0;
+  for (int r = 0; r < m; ++r)
+    ineq += W->hi[r] * (dy[r] > 0.0 ? dy[r] : 0.0) + W->lo[r] * (dy[r] < 0.0 ? dy[r] : 0.0);
+  if (!(ineq < eps * norm)) return 0;
+  double* aty = W->tmpn2;
+  mat_tvec(W, dy, aty);
+  double na = 0.0;
+  for (int c = 0; c < n; ++c) { double a = fabs(aty[c] / W->D[c]); if (a > na) na = a; }
+  return na < eps * norm;
+}
+
+/* osqp 0.6 auxil.c is_dual_infeasible, on the last iteration's delta_x:
+ * ||D dx|| > 0, q'dx < c eps ||D dx|| (q = 0), ||D^-1 P dx|| < c eps ||D dx|| and
+ * every row with a finite bound keeps (E^-1 A dx) on its side within eps ||D dx||. */
+static int is_dual_infeasible(Work* W, double eps) {
+  const int m = W->m, n = W->n;
+  const double* dx = W->dx;
+  double norm = 0.0;
+  for (int c = 0; c < n; ++c) { double a = fabs(W->D[c] * dx[c]); if (a > norm) norm = a; }
+  if (!(norm > DIV_TOL)) return 0;
+  if (!(0.0 < W->c * eps * norm)) return 0; /* q'dx = 0 */
+  double np_ = 0.0;
+  for (int c = 0; c < n; ++c) { double a = fabs(W->Pd[c] * dx[c] / W->D[c]); if (a > np_) np_ = a; }
+  if (!(np_ < W->c * eps * norm)) return 0;
+  double* adx = W->tmpm2;
+  mat_vec(W, dx, adx);
+  for (int r = 0; r < m; ++r) {
+    const double v = adx[r] / W->E[r];
+    if ((W->hi[r] < OSQP_INFTY * MIN_SCALING && v > eps * norm) ||
+        (W->lo[r] > -OSQP_INFTY * MIN_SCALING && v < -eps * norm))
+      return 0;
+  }
+  return 1;
+}
+
+/* osqp 0.6 check_termination: solved, else primal, else dual infeasible (each
+ * infeasibility test only where its residual test failed); approximate = the
+ * x10 tolerances of the max_iter exit.  Returns the status or 0. */
+static int check_termination(Work* W, const Info* I, const mpcq_params* p, int approximate) {
+  const double f = approximate ? 10.0 : 1.0;
+  const int pri_ok = I->pri_res < f * I->eps_pri, dua_ok = I->dua_res < f * I->eps_dua;
+  const int pinf = !pri_ok && is_primal_infeasible(W, f * p->eps_prim_inf);
+  const int dinf = !dua_ok && is_dual_infeasible(W, f * p->eps_dual_inf);
+  if (pri_ok && dua_ok) return approximate ? MPCQ_STATUS_SOLVED_INACCURATE : MPCQ_STATUS_SOLVED;
+  if (pinf) return approximate ? MPCQ_STATUS_PRIMAL_INFEASIBLE_INACCURATE : MPCQ_STATUS_PRIMAL_INFEASIBLE;
+  if (dinf) return approximate ? MPCQ_STATUS_DUAL_INFEASIBLE_INACCURATE : MPCQ_STATUS_DUAL_INFEASIBLE;
+  return 0;
+}
+
 /* ---- polish (OSQP 0.6 polish.c restated in reduced form) ----------------
  * One round = OSQP's polish: guess the active set from (z, y) (lower-active if
  * z - l < -y, upper-active if u - z < y), solve the equality-constrained QP
@@ -694,13 +772,16 @@ int oracle_qp_solve(const mpcq_params* p, int N, const double* Ax, const double*
   memcpy(W->A, Ax, 8 * (size_t)W->nnz);
   int finite = 1;
   for (int q = 0; q < W->nnz; ++q) if (!isfinite(Ax[q])) finite = 0;
+  int ordered = 1;
   for (int r = 0; r < m; ++r) {
     double lo = l[r] < -OSQP_INFTY ? -OSQP_INFTY : l[r];
     double hi = u[r] > OSQP_INFTY ? OSQP_INFTY : u[r];
     if (isnan(lo) || isnan(hi)) finite = 0;
+    if (lo > hi) ordered = 0; /* osqp validate_data / osqp_update_bounds reject l > u */
     W->lo[r] = lo; W->hi[r] = hi;
   }
   if (!finite) { st = MPCQ_STATUS_NONFINITE; goto out; }
+  if (!ordered) { st = MPCQ_STATUS_BAD_BOUNDS; goto out; }
   if (p->scaling > 0) scale_data(W, p->scaling);
   else { for (int c = 0; c < n; ++c) W->D[c] = 1.0; for (int r = 0; r < m; ++r) W->E[r] = 1.0; W->c = 1.0; }
   for (int r = 0; r < m; ++r) { W->lo[r] *= W->E[r]; W->hi[r] *= W->E[r]; }
@@ -711,7 +792,8 @@ int oracle_qp_solve(const mpcq_params* p, int N, const double* Ax, const double*
     for (int c = 0; c < n; ++c) W->x[c] = warm_x[c] / W->D[c];
     mat_vec(W, W->x, W->z);
   }
-  if (warm_y) for (int r = 0; r < m; ++r) W->y[r] = W->c * warm_y[r] / W->E[r];
+  if (warm_y)  /* dual_warm = 1: osqp's workspace y, kept as is; 0: osqp_warm_start_y scaling */
+    for (int r = 0; r < m; ++r) W->y[r] = p->dual_warm ? warm_y[r] : W->c * warm_y[r] / W->E[r];
   if (bt_factor(W, p->sigma, W->rho) != 0) { st = MPCQ_STATUS_FACTOR_FAILED; goto out; }
   Info I;
   memset(&I, 0, sizeof(I));
@@ -725,19 +807,23 @@ int oracle_qp_solve(const mpcq_params* p, int N, const double* Ax, const double*
     for (int c = 0; c < n; ++c) W->rhs[c] += p->sigma * W->xp[c]; /* - q, q = 0 */
     bt_solve(W, W->rhs, W->xt);
     mat_vec(W, W->xt, W->zt);
-    for (int c = 0; c < n; ++c) W->x[c] = p->alpha * W->xt[c] + (1.0 - p->alpha) * W->xp[c];
+    for (int c = 0; c < n; ++c) {
+      W->x[c] = p->alpha * W->xt[c] + (1.0 - p->alpha) * W->xp[c];
+      W->dx[c] = W->x[c] - W->xp[c]; /* osqp update_x: delta_x */
+    }
     for (int r = 0; r < m; ++r) {
       double zr = p->alpha * W->zt[r] + (1.0 - p->alpha) * W->zp[r];
       double t = zr + (1.0 / W->rho[r]) * W->y[r]; /* osqp: rho_inv_vec .* y */
       double zz = t < W->lo[r] ? W->lo[r] : (t > W->hi[r] ? W->hi[r] : t);
-      W->y[r] = W->y[r] + W->rho[r] * (zr - zz);
+      W->dy[r] = W->rho[r] * (zr - zz); /* osqp update_y: delta_y */
+      W->y[r] = W->y[r] + W->dy[r];
       W->z[r] = zz;
     }
     can_check = p->check_termination > 0 && (iter % p->check_termination == 0);
     if (can_check) {
       update_info(W, W->x, W->z, W->y, p, &I);
       if (!(isfinite(I.pri_res) && isfinite(I.dua_res))) { st = MPCQ_STATUS_NONFINITE; break; }
-      if (check_term(&I, p, 0)) { st = MPCQ_STATUS_SOLVED; break; }
+      if ((st = check_termination(W, &I, p, 0)) != 0) break;
     }
     if (p->adaptive_rho && p->adaptive_rho_interval > 0 && iter % p->adaptive_rho_interval == 0) {
       if (!can_check) update_info(W, W->x, W->z, W->y, p, &I);
@@ -755,9 +841,10 @@ int oracle_qp_solve(const mpcq_params* p, int N, const double* Ax, const double*
   if (st == 0) {
     if (!can_check) {
       update_info(W, W->x, W->z, W->y, p, &I);
-      if (check_term(&I, p, 0)) st = MPCQ_STATUS_SOLVED;
+      st = check_termination(W, &I, p, 0);
     }
-    if (st == 0) st = check_term(&I, p, 1) ? MPCQ_STATUS_SOLVED_INACCURATE : MPCQ_STATUS_MAX_ITER_REACHED;
+    if (st == 0) st = check_termination(W, &I, p, 1);
+    if (st == 0) st = MPCQ_STATUS_MAX_ITER_REACHED;
   }
   /* polish == 1: OSQP (only after SOLVED); polish == 2: also after an inaccurate
    * or max-iter exit, upgrading the status when the polished point meets eps. */
@@ -773,9 +860,15 @@ int oracle_qp_solve(const mpcq_params* p, int N, const double* Ax, const double*
   }
 out:
   if (x_out) for (int c = 0; c < n; ++c) x_out[c] = W->D[c] * W->x[c];
-  if (y_out) for (int r = 0; r < m; ++r) y_out[r] = W->E[r] * W->y[r] / W->c;
-  if (st == MPCQ_STATUS_NONFINITE || st == MPCQ_STATUS_FACTOR_FAILED) {
+  if (y_out) for (int r = 0; r < m; ++r) y_out[r] = p->dual_warm ? W->y[r] : W->E[r] * W->y[r] / W->c;
+  if (st == MPCQ_STATUS_NONFINITE || st == MPCQ_STATUS_FACTOR_FAILED || st == MPCQ_STATUS_BAD_BOUNDS) {
     if (x_out) for (int c = 0; c < n; ++c) x_out[c] = NAN;
+  }
+  if (st == MPCQ_STATUS_PRIMAL_INFEASIBLE || st == MPCQ_STATUS_DUAL_INFEASIBLE ||
+      st == MPCQ_STATUS_PRIMAL_INFEASIBLE_INACCURATE || st == MPCQ_STATUS_DUAL_INFEASIBLE_INACCURATE) {
+    /* osqp store_solution: no solution, x = y = NaN (and a cold start next time) */
+    if (x_out) for (int c = 0; c < n; ++c) x_out[c] = NAN;
+    if (y_out) for (int r = 0; r < m; ++r) y_out[r] = NAN;
   }
   if (status) *status = st;
   if (iters) *iters = it_done;

@@ -42,6 +42,8 @@ class Params(C.Structure):
         ("eps_rel", C.c_double),
         ("adaptive_rho_tolerance", C.c_double),
         ("delta", C.c_double),
+        ("eps_prim_inf", C.c_double),
+        ("eps_dual_inf", C.c_double),
         ("max_iter", C.c_int32),
         ("check_termination", C.c_int32),
         ("adaptive_rho", C.c_int32),
@@ -50,7 +52,8 @@ class Params(C.Structure):
         ("polish", C.c_int32),
         ("polish_refine_iter", C.c_int32),
         ("polish_rounds", C.c_int32),
-        ("reserved", C.c_int32 * 8),
+        ("dual_warm", C.c_int32),
+        ("reserved", C.c_int32 * 7),
     ]
 
 
@@ -103,10 +106,16 @@ def _bind(path: str):
 
 
 def lib():
-    """The checker build (-O2 -ffp-contract=off: the rounding the parity tests pin)."""
+    """The checker build (-O2 -ffp-contract=off: the rounding the parity tests pin).
+    MPCQ_ORACLE_ASAN=1 loads the AddressSanitizer + UBSan build instead (make asan;
+    the process needs libasan preloaded: tests/test_oracle_asan.py does that)."""
     if "check" not in _libs:
-        build()
-        _libs["check"] = _bind(_LIB_PATH)
+        if os.environ.get("MPCQ_ORACLE_ASAN") == "1":
+            subprocess.run(["make", "-s", "-C", _HERE, "asan"], check=True)
+            _libs["check"] = _bind(os.path.join(_HERE, "liboracle_asan.so"))
+        else:
+            build()
+            _libs["check"] = _bind(_LIB_PATH)
     return _libs["check"]
 
 

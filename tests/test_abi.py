@@ -37,7 +37,7 @@ def test_exports_every_declared_symbol(mpcq):
 
 
 def test_abi_version(mpcq):
-    assert mpcq.lib().mpcq_abi_version() == 1
+    assert mpcq.lib().mpcq_abi_version() == 2
 
 
 def test_default_params_match_reference(mpcq, golden16, oracle):
@@ -56,6 +56,7 @@ def test_default_params_match_reference(mpcq, golden16, oracle):
     assert (p.rho, p.sigma, p.alpha) == (0.1, 1e-6, 1.6)
     assert (p.eps_abs, p.eps_rel) == (1e-7, 1e-7)
     assert (p.max_iter, p.check_termination, p.scaling, p.polish) == (4000, 25, 10, 0)
+    assert (p.eps_prim_inf, p.eps_dual_inf, p.dual_warm) == (1e-4, 1e-4, 0)
     # same constants as the oracle's restatement
     o = oracle.default_params()
     for name, _ in p._fields_:

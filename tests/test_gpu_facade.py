@@ -13,7 +13,8 @@ TOL = 1e-8  # |x_gpu - x_oracle| per tick (same iterations; fp64 rounding only)
 def test_closed_loop_matches_oracle(golden16, oracle):
     from mpcq.wrapper import MPC_Wrapper
     w_gpu = MPC_Wrapper(0.02, 16, 20, 0.32, device=0)
-    w_ora = MPC_Wrapper(0.02, 16, 20, 0.32, engine=OracleEngine(oracle))
+    w_ora = MPC_Wrapper(0.02, 16, 20, 0.32, engine=OracleEngine(oracle, dual_warm=1))
+    assert w_gpu.mpc.engine.params.dual_warm == 1  # the façade carries osqp's scaled y
     assert w_gpu.get_latest_result().tolist() == [0.0, 0.0, 8.0] * 4
     for tick in range(5):
         b = tick % 3

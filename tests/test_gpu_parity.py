@@ -218,3 +218,69 @@ def test_polish_osqp_default_mode(golden16, oracle, mpcq):
     print(f"polish=1: accepted on {acc_gpu}/{B} (oracle {acc_ora}/{B}), accepted max|f - f*| {worst:.2e}")
     assert acc_gpu >= acc_ora
     assert worst < 1e-8
+
+
+def test_infeasibility_and_bad_bounds_vs_oracle(eng16, golden16, oracle, mpcq):
+    """OSQP 0.6's primal-infeasibility detection (a swing force held at 0 and asked
+    for fz >= 10 N) and l > u rejection: statuses (-3 / -13) and iteration counts
+    equal to the oracle's on every instance, x NaN as osqp's store_solution, and
+    the untouched feasible instances of the same launch unaffected; then
+    max_iter around the detection point (MAX_ITER_REACHED vs -3 at the final
+    check) in the engine's own launches."""
+    from test_infeasibility import infeasible_instance
+    N = 16
+    Ax, L, U, kinds = [], [], [], []
+    for b in range(0, 50, 3):
+        inst = infeasible_instance(golden16, b)
+        if inst is not None:
+            Ax.append(inst[0]); L.append(inst[1]); U.append(inst[2]); kinds.append("infeasible")
+        Ax.append(golden16["Ax"][b]); L.append(golden16["l"][b]); U.append(golden16["u"][b]); kinds.append("ok")
+    lb = golden16["l"][1].copy()
+    lb[24 * N + 3] = 1.0  # friction row with u = 0 < l
+    Ax.append(golden16["Ax"][1]); L.append(lb); U.append(golden16["u"][1]); kinds.append("l>u")
+    Ax, L, U = np.array(Ax), np.array(L), np.array(U)
+    r = eng16.qp_solve(Ax, L, U)
+    for i, kind in enumerate(kinds):
+        o = oracle.qp_solve(N, Ax[i], L[i], U[i])
+        assert r["status"][i] == o["status"], (i, kind, r["status"][i], o["status"])
+        assert r["iters"][i] == o["iters"], (i, kind, r["iters"][i], o["iters"])
+        want = {"infeasible": mpcq.STATUS_PRIMAL_INFEASIBLE, "ok": mpcq.STATUS_SOLVED,
+                "l>u": mpcq.STATUS_BAD_BOUNDS}[kind]
+        assert r["status"][i] == want, (i, kind)
+        if kind == "ok":
+            assert np.abs(r["x"][i] - o["x"]).max() < X_TOL
+        else:
+            assert np.isnan(r["x"][i]).all()
+    inf_idx = [i for i, k in enumerate(kinds) if k == "infeasible"][:4]
+    for mi in (60, 100, 101, 110):
+        with mpcq.Engine(16, max_iter=mi) as e:
+            rr = e.qp_solve(Ax[inf_idx], L[inf_idx], U[inf_idx])
+        po = oracle.default_params(max_iter=mi)
+        for j, i in enumerate(inf_idx):
+            o = oracle.qp_solve(N, Ax[i], L[i], U[i], params=po)
+            assert rr["status"][j] == o["status"] and rr["iters"][j] == o["iters"], (mi, i)
+
+
+@pytest.mark.parametrize("dual_warm", [0, 1])
+def test_dual_warm_vs_oracle(golden16, oracle, mpcq, dual_warm):
+    """Two ticks per instance: a cold solve of QP a, then QP b warm-started from it
+    (x, y, rho) under both dual carry-overs; iterations equal to the oracle's and
+    x within W_TOL, y within Y_RTOL relative on every instance (observed 2e-9 and
+    1.6e-8: the warm start carries the first solve's rounding into the second, and
+    ADMM's duals converge more slowly than its primal)."""
+    W_TOL, Y_RTOL = 1e-8, 1e-6
+    g, N = golden16, 16
+    B = 24
+    a_idx, b_idx = np.arange(B), (np.arange(B) + 7) % g["Ax"].shape[0]
+    with mpcq.Engine(N, dual_warm=dual_warm) as e:
+        r1 = e.qp_solve(g["Ax"][a_idx], g["l"][a_idx], g["u"][a_idx])
+        r2 = e.qp_solve(g["Ax"][b_idx], g["l"][b_idx], g["u"][b_idx], warm_x=r1["x"], warm_y=r1["y"],
+                        rho=r1["rho"])
+    p = oracle.default_params(dual_warm=dual_warm)
+    for i in range(B):
+        o1 = oracle.qp_solve(N, g["Ax"][a_idx[i]], g["l"][a_idx[i]], g["u"][a_idx[i]], params=p)
+        o2 = oracle.qp_solve(N, g["Ax"][b_idx[i]], g["l"][b_idx[i]], g["u"][b_idx[i]], params=p,
+                             warm_x=o1["x"], warm_y=o1["y"], rho=o1["rho"])
+        assert r2["iters"][i] == o2["iters"], (i, r2["iters"][i], o2["iters"])
+        assert np.abs(r2["x"][i] - o2["x"]).max() < W_TOL
+        assert np.abs(r2["y"][i] - o2["y"]).max() < Y_RTOL * max(1.0, np.abs(o2["y"]).max())

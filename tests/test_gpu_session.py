@@ -66,16 +66,17 @@ def _compare(sess, ors, mpcq, k, agree, plan_tol=1e-15, x_rtol=0.0):
     return float(np.abs(f0 - np.stack([o.f0 for o in ors])).max()), it
 
 
-@pytest.mark.parametrize("N", [8, 16, 24, 32])
-def test_session_host_inputs_vs_oracle(mpcq, N):
-    """Measured states from the host each tick (the reference's interface)."""
+@pytest.mark.parametrize("N,dual_warm", [(8, 0), (16, 0), (16, 1), (24, 1), (32, 0)])
+def test_session_host_inputs_vs_oracle(mpcq, N, dual_warm):
+    """Measured states from the host each tick (the reference's interface), with
+    either dual carry-over (dual_warm = 1: osqp's scaled workspace y)."""
     from oracle import oracle as O
     B, T = 12, 6
     gaits = _gaits(B, N)
     rng = np.random.default_rng(11 + N)
     agree, worst = [], 0.0
-    with mpcq.Engine(N) as eng, mpcq.Session(eng, B, gait0=gaits) as sess:
-        ors = [O.Session(N, gaits[b]) for b in range(B)]
+    with mpcq.Engine(N, dual_warm=dual_warm) as eng, mpcq.Session(eng, B, gait0=gaits) as sess:
+        ors = [O.Session(N, gaits[b], params=O.default_params(dual_warm=dual_warm)) for b in range(B)]
         for k in range(T):
             state, l_feet, v_ref = _inputs(rng, B, k)
             red = (np.arange(B) % 5 == 0).astype(np.int32)

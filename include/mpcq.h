@@ -158,12 +158,14 @@ int mpcq_qp_solve_batch(mpcq_ctx* ctx, int64_t batch, const double* Ax,
 
 /* ---- fused hot path --------------------------------------------------------
  * Replaces MPC.run(k, xref, fsteps) (MPC.py:460-514) for a batch: formulation
- * + OSQP solve + retrieve_result (MPC.py:432-458) in one launch.
- * f0 [B][12] = f_applied; x [B][n] optional; y [B][m] optional. */
+ * + OSQP solve (with the osqp workspace carried between ticks: warm_x, warm_y,
+ * rho_in, as mpcq_qp_solve_batch) + retrieve_result (MPC.py:432-458) in one
+ * launch.  f0 [B][12] = f_applied; x [B][n], y [B][m], rho_out [B] optional. */
 int mpcq_solve_batch(mpcq_ctx* ctx, int64_t batch, const double* xref,
                      const double* fsteps, int mode, const double* warm_x,
-                     const double* warm_y, double* f0, double* x, double* y,
-                     int32_t* status, int32_t* iters, int32_t* info, uint32_t flags);
+                     const double* warm_y, const double* rho_in, double* f0, double* x,
+                     double* y, double* rho_out, int32_t* status, int32_t* iters,
+                     int32_t* info, uint32_t flags);
 
 /* ---- footstep planner ------------------------------------------------------
  * The producer of (xref, fsteps): FootstepPlanner.py.  Per instance the

@@ -397,12 +397,13 @@ int mpcq_qp_solve_batch(mpcq_ctx* c, int64_t B, const double* Ax, const double* 
 }
 
 int mpcq_solve_batch(mpcq_ctx* c, int64_t B, const double* xref, const double* fsteps, int mode,
-                     const double* warm_x, const double* warm_y, double* f0, double* x, double* y,
-                     int32_t* status, int32_t* iters, int32_t* info, uint32_t flags) {
+                     const double* warm_x, const double* warm_y, const double* rho_in, double* f0,
+                     double* x, double* y, double* rho_out, int32_t* status, int32_t* iters,
+                     int32_t* info, uint32_t flags) {
   if (!xref || !fsteps) return fail(MPCQ_E_INVALID, "xref, fsteps are required");
   if (mode != MPCQ_MODE_UPDATE && mode != MPCQ_MODE_SETUP) return fail(MPCQ_E_INVALID, "bad mode");
   return solve_common(c, B, true, xref, fsteps, mode, nullptr, nullptr, nullptr, warm_x, warm_y,
-                      nullptr, f0, x, y, status, iters, nullptr, info, flags);
+                      rho_in, f0, x, y, status, iters, rho_out, info, flags);
 }
 
 // FootstepPlanner constants (FootstepPlanner.py:18-52, 316-322, 376; processing.py:131).

@@ -193,8 +193,8 @@ def lib():
     L.mpcq_formulate_batch.argtypes = [vp, C.c_int64, vp, vp, C.c_int, vp, vp, vp, vp, C.c_uint32]
     L.mpcq_qp_solve_batch.argtypes = [vp, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                       vp, C.c_uint32]
-    L.mpcq_solve_batch.argtypes = [vp, C.c_int64, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp,
-                                   C.c_uint32]
+    L.mpcq_solve_batch.argtypes = [vp, C.c_int64, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                   vp, C.c_uint32]
     L.mpcq_debug_set_stamps.argtypes = [vp, vp]
     L.mpcq_default_planner_params.argtypes = [C.POINTER(PlannerParams)]
     L.mpcq_default_planner_params.restype = None

@@ -133,20 +133,24 @@ class Engine:
                                             _p(x), _p(y), _p(st), _p(it), _p(ro), _p(info), 0)
         return dict(x=x, y=y, status=st, iters=it, rho=ro, rho_updates=info[:, 0], polish=info[:, 1])
 
-    def solve(self, xref, fsteps, mode: int = L.MODE_UPDATE, warm_x=None, warm_y=None,
+    def solve(self, xref, fsteps, mode: int = L.MODE_UPDATE, warm_x=None, warm_y=None, rho=None,
               want_x: bool = True, want_y: bool = False):
+        """Fused formulation + solve (mpcq_solve_batch): MPC.run's QP for a batch, with
+        the osqp workspace of the previous tick (warm_x, warm_y, rho) when given."""
         xref, fsteps, B = self._batch_inputs(xref, fsteps)
         wx = None if warm_x is None else _f64(warm_x).reshape(B, self.n)
         wy = None if warm_y is None else _f64(warm_y).reshape(B, self.m)
+        rin = None if rho is None else np.ascontiguousarray(np.broadcast_to(np.asarray(rho, np.float64), (B,)))
         f0 = np.empty((B, 12))
         x = np.empty((B, self.n)) if want_x else None
         y = np.empty((B, self.m)) if want_y else None
+        rout = np.empty(B)
         st = np.empty(B, np.int32)
         it = np.empty(B, np.int32)
         info = np.empty((B, 4), np.int32)
-        self._call("mpcq_solve_batch", self._h, B, _p(xref), _p(fsteps), mode, _p(wx), _p(wy), _p(f0),
-                                         _p(x), _p(y), _p(st), _p(it), _p(info), 0)
-        return dict(f0=f0, x=x, y=y, status=st, iters=it, rho_updates=info[:, 0], polish=info[:, 1])
+        self._call("mpcq_solve_batch", self._h, B, _p(xref), _p(fsteps), mode, _p(wx), _p(wy), _p(rin), _p(f0),
+                                         _p(x), _p(y), _p(rout), _p(st), _p(it), _p(info), 0)
+        return dict(f0=f0, x=x, y=y, rho=rout, status=st, iters=it, rho_updates=info[:, 0], polish=info[:, 1])
 
     # ------------------------------------------------------------------ footstep planner
     def plan(self, ops: int, k: int, state, l_feet, v_ref, gait, rot_flag, h_rot, xref, fsteps,
@@ -201,7 +205,7 @@ class Engine:
         flags = L.FLAG_DEVICE_PTRS | (L.FLAG_ASYNC if asynchronous else 0)
         v = lambda q: C.c_void_p(q) if q else None  # noqa: E731
         self._call("mpcq_solve_batch", self._h, int(batch), v(xref_ptr), v(fsteps_ptr), mode, v(warm_x_ptr),
-                                         v(warm_y_ptr), v(f0_ptr), v(x_ptr), v(y_ptr), v(status_ptr),
+                                         v(warm_y_ptr), None, v(f0_ptr), v(x_ptr), v(y_ptr), None, v(status_ptr),
                                          v(iters_ptr), v(info_ptr), flags)
 
     def last_kernel_ms(self):

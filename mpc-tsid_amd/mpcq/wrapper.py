@@ -14,8 +14,11 @@ Mirrors, name for name, what the reference's control loop touches:
   ``solve_batch(xref[B,12,N+1], fsteps[B,20,13]) -> f0[B,12]``.
 * ``MPC_Virtual(mpc_type, dt_mpc, n_steps, k_mpc, T_gait)`` -- MPC_Virtual.py:20-35.
 
-The tick path is formulate (MPC.update_ML / update_NK, or create_* at k == 0)
-then the OSQP-0.6 solve with the reference's warm start (MPC.py:403-406): x is
+A tick is one fused launch (mpcq_solve_batch): the formulation (MPC.update_ML /
+update_NK, or create_* at k == 0) and the OSQP-0.6 solve with the reference's warm
+start (MPC.py:403-406) -- no host round trip between them.  ``ML`` / ``NK`` /
+``NK_inf`` (MPC.py:151-234; nothing downstream reads them) are formed on first
+access from the tick's inputs by a separate formulation launch.  x is
 the previous solution shifted by one stage (states: last stage zeroed; forces:
 wrapped, as np.roll does), y and rho carry over from the previous solve as the
 osqp workspace does.  The dual is carried the way osqp 0.6 carries it
@@ -69,9 +72,8 @@ class MPC:
         self.P = sp.diags(diag).tocsc()
         self.Q = np.zeros((24 * N,))
         self._indptr, self._indices = pattern(N)
-        self.ML = None
-        self.NK = None
-        self.NK_inf = None
+        self._form = None      # (xref, fsteps, mode) of the last tick, for ML / NK on demand
+        self._form_cache = None
         self.x_robot = np.zeros((12, N))
         self.f_applied = np.zeros((12,))
         self.q_next = np.zeros((6, 1))
@@ -102,21 +104,18 @@ class MPC:
         self.xref = xref
         self.x0 = xref[:, 0:1]
         mode = L.MODE_SETUP if k == 0 else L.MODE_UPDATE
-        form = self.engine.formulate(xref, fsteps, mode)
-        if form["status"][0] == L.STATUS_BAD_GAIT:
+        xr = np.ascontiguousarray(xref)[None]
+        fs = np.array(fsteps, dtype=np.float64, copy=True)[None]
+        if k == 0:
+            r = self.engine.solve(xr, fs, mode, want_x=True, want_y=True)
+        else:
+            r = self.engine.solve(xr, fs, mode, warm_x=self._warm_x(), warm_y=self._y, rho=self._rho,
+                                  want_x=True, want_y=True)
+        if r["status"][0] == L.STATUS_BAD_GAIT:
             raise ValueError("fsteps: gait table needs a zero-duration terminator and durations summing to n_steps")
+        self._form, self._form_cache = (xr, fs, mode), None
         if k > 0:
             fsteps[np.isnan(fsteps)] = 0.0  # MPC.py:327, the caller's array is mutated
-        import scipy.sparse as sp
-        n, m = 24 * self.n_steps, 44 * self.n_steps
-        self.ML = sp.csc_matrix((form["Ax"][0], self._indices, self._indptr), shape=(m, n))
-        self.NK = form["u"][0].reshape(-1, 1)
-        self.NK_inf = form["l"][0].copy()
-        if k == 0:
-            r = self.engine.qp_solve(form["Ax"], form["l"], form["u"])
-        else:
-            r = self.engine.qp_solve(form["Ax"], form["l"], form["u"], warm_x=self._warm_x(),
-                                     warm_y=self._y, rho=self._rho)
         self.status = int(r["status"][0])
         self.iters = int(r["iters"][0])
         self.x = r["x"][0]
@@ -131,6 +130,36 @@ class MPC:
         self.q_w[3:5, 0] = self.q_next[3:5, 0]
         self.q_w[5, 0] += self.q_next[5, 0]
         return 0
+
+    def _formulation(self):
+        if self._form is None:
+            return None
+        if self._form_cache is None:
+            xr, fs, mode = self._form
+            form = self.engine.formulate(xr, fs, mode)
+            import scipy.sparse as sp
+            n, m = 24 * self.n_steps, 44 * self.n_steps
+            self._form_cache = (sp.csc_matrix((form["Ax"][0], self._indices, self._indptr), shape=(m, n)),
+                                form["u"][0].reshape(-1, 1), form["l"][0].copy())
+        return self._form_cache
+
+    @property
+    def ML(self):
+        """A of the last tick's QP (MPC.py:151), CSC in the reference's pattern."""
+        f = self._formulation()
+        return None if f is None else f[0]
+
+    @property
+    def NK(self):
+        """u of the last tick's QP as a column (MPC.py:192-234)."""
+        f = self._formulation()
+        return None if f is None else f[1]
+
+    @property
+    def NK_inf(self):
+        """l of the last tick's QP (MPC.py:226-232, 410)."""
+        f = self._formulation()
+        return None if f is None else f[2]
 
     def retrieve_result(self):
         """MPC.py:432-458."""

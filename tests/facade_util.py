@@ -23,6 +23,17 @@ class OracleEngine:
             Ax, l, u, st = np.zeros(nnz), np.zeros(m), np.zeros(m), -11
         return dict(Ax=Ax[None], l=l[None], u=u[None], status=np.array([st], np.int32))
 
+    def solve(self, xref, fsteps, mode=0, warm_x=None, warm_y=None, rho=None, want_x=True, want_y=True):
+        """The fused tick (formulate + qp_solve) on the oracle, Engine.solve's signature."""
+        f = self.formulate(xref[0], fsteps[0], mode)
+        if f["status"][0] != 0:
+            n, m = 24 * self.n_steps, 44 * self.n_steps
+            return dict(f0=np.full((1, 12), np.nan), x=np.full((1, n), np.nan), y=np.full((1, m), np.nan),
+                        rho=np.array([np.nan]), status=f["status"], iters=np.zeros(1, np.int32))
+        r = self.qp_solve(f["Ax"], f["l"], f["u"], warm_x, warm_y, rho)
+        r["f0"] = r["x"][:, 12 * self.n_steps:12 * self.n_steps + 12]
+        return r
+
     def qp_solve(self, Ax, l, u, warm_x=None, warm_y=None, rho=None):
         self.calls.append(dict(warm_x=None if warm_x is None else np.array(warm_x),
                                warm_y=None if warm_y is None else np.array(warm_y), rho=rho))

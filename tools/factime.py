@@ -11,7 +11,7 @@ B=1024
 f0 = np.empty((B, 12)); st = np.empty(B, np.int32); it = np.empty(B, np.int32)
 xr = np.ascontiguousarray(src["xref"]); fs = np.ascontiguousarray(src["fsteps"])
 p = lambda a: a.ctypes.data_as(C.c_void_p)
-L.check(L.lib().mpcq_solve_batch(eng._h, B, p(xr), p(fs), 1, None, None, p(f0), None, None, p(st), p(it), p(info), 0))
+L.check(L.lib().mpcq_solve_batch(eng._h, B, p(xr), p(fs), 1, None, None, None, p(f0), None, None, None, p(st), p(it), p(info), 0))
 fc = info[:, 2].astype(np.float64) * 256
 nf = info[:, 0] + 1
 per = fc / nf

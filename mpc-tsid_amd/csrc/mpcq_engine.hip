@@ -82,6 +82,18 @@ __device__ __forceinline__ int FO(int k, int f, int c) {  // force column f_k[3f
 // lane (within the stage row) that owns force / state index psi = 3f + c
 __host__ __device__ constexpr int LN(int psi) { return 4 * (psi / 3) + psi % 3; }
 
+// Step-ordered slots of the sweep arrays.  The top chain walks stages 0, 1, ..
+// upwards and the bottom chain N-1, N-2, .. downwards; storing the bottom
+// stages in reverse (stage k > MID at slot N + MID - k) makes both chains walk
+// their slots in the same direction, so every lane of the sweep wave addresses
+// step j as (its own base) + j * (a uniform stride): an immediate offset, no
+// per-step pointer arithmetic.  SIG: G/H, S^-1 and the right-hand sides
+// (stages 0..N-1); SIGX: the state vectors xs[q] = X_q, q = 0..N.
+template <int N>
+__device__ __forceinline__ int SIG(int k) { return k <= N / 2 ? k : N + N / 2 - k; }
+template <int N>
+__device__ __forceinline__ int SIGX(int q) { return q <= N / 2 ? q : N + N / 2 + 1 - q; }
+
 // ---------------------------------------------------------------------------
 // cross-lane helpers
 
@@ -392,12 +404,13 @@ constexpr int RS = 12, GS = 12 * RS;
 template <int N>
 struct Smem {
   double Ab[126 * N - 18];  // scaled constraint values, CSC order
-  // GH[0] = M^{-1}, GH[k] = G_k (1 <= k <= m), GH[k] = H_{k-1} (k > m), row-major.
+  // GH[0] = M^{-1}, GH[SIG(k)] = G_k (1 <= k <= m), GH[SIG(k+1)] = H_k (m <= k < N-1),
+  // row-major (the sweeps' step order, see SIG).
   // During the factorisation slot k holds Q_k [0,36), F_k W_k [36,108) and the
   // dynamics-row rho of stage k [108,120); during scaling the row factors; in
   // the prologue xref / fsteps / the gait walk.
   alignas(16) double GH[N][GS];
-  alignas(16) double Sm[N][GS];         // S_k^{-1} / U_k^{-1} of stage k, row-major (row stride RS)
+  alignas(16) double Sm[N][GS];         // S_k^{-1} / U_k^{-1} of stage k at SIG(k), row-major (row stride RS)
   double FWs[N][72];        // F_k W_k (12x6, row psi at [6 psi]); W_k = B_k' R on rows 6..11
   double QL[N][36];         // B_k F_k W_k = R^{-1} W_k' F_k W_k (6x6)
   union {
@@ -414,7 +427,8 @@ struct Smem {
       double St[144], Sb[144];  // sweep hand-offs of the factorisation
     } fa;
   } u;
-  double red[12 * N];  // per-row partial reductions
+  // per-row partial reductions; during the sweeps the sink of lanes whose store is void
+  double red[(12 * N > 12 * (N / 2 + 1) + 64) ? 12 * N : 12 * (N / 2 + 1) + 64];
   double dump[16 * N];      // per-lane sink: predicated stores write here instead of branching
   double zero[72];          // zeros: masked coefficient reads point here instead of selecting
   int flag[4];
@@ -904,7 +918,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           asm volatile("" ::: "memory");
         }
         if (cl) {
-          double* const Gd = &sh.GH[upper ? k : k + 1][RS * ph];
+          double* const Gd = &sh.GH[upper ? SIG<N>(k) : SIG<N>(k + 1)][RS * ph];
 #pragma unroll
           for (int ci = 0; ci < 12; ++ci) Gd[ci] = -G[ci];  // stored negated
         }
@@ -927,7 +941,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           gj12(Ro, ph, ok);
           if (cl) {
 #pragma unroll
-            for (int ci = 0; ci < 12; ++ci) sh.Sm[k][RS * ph + ci] = Ro[ci];
+            for (int ci = 0; ci < 12; ++ci) sh.Sm[SIG<N>(k)][RS * ph + ci] = Ro[ci];
           }
           wave_sync();  // the previous inverse has been consumed by this row
           if (cl) {
@@ -961,7 +975,10 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     const int oF4 = FO<N>(k, f, 2) + 9;
     const int oFW = 72 * k + 6 * ph, oFWc = 72 * k + (isv ? ph - 6 : 0);
     const int oQL = 36 * k + 6 * (isv ? ph - 6 : 0);
-    const int oXS = 12 * (k + 1) + ph, oXSp = 12 * k + ph, oXSp6 = 12 * k + (ph < 6 ? ph + 6 : ph);
+    const int oXSp = 12 * k + ph, oXSp6 = 12 * k + (ph < 6 ? ph + 6 : ph);  // natural order (update_info)
+    // the sweep's states in its slots (SIGX): own X_{k+1}, the previous stage's X_k
+    const int rXS = 12 * SIGX<N>(k + 1) + ph, rXSp = 12 * SIGX<N>(k) + ph,
+              rXSp6 = 12 * SIGX<N>(k) + (ph < 6 ? ph + 6 : ph);
     const double m2 = cc == 2 ? 1.0 : 0.0;
     // masked variants for the loop: a lane whose term is structurally absent reads a
     // zero (stage 0 has no previous stage; H6 only on the position rows; the force Schur
@@ -971,9 +988,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     const int oFWcm = isv ? oFWc : (int)(sh.zero - &sh.FWs[0][0]);
     const int oQLm = isv ? oQL : (int)(sh.zero - &sh.QL[0][0]);
     lds_cd* XSr = (lds_cd*)&sh.u.it.xs[0][0];
-    double* const Wbo = &sh.u.it.bo[k][ph];
-    double* const Wna = &sh.u.it.na[hp ? k - 1 : N - 1][ph];
-    double* const Wnb = &sh.u.it.nb[hp ? k - 1 : N - 1][hp ? (ph < 6 ? ph + 6 : ph - 6) : ph];
+    double* const Wbo = &sh.u.it.bo[SIG<N>(k)][ph];
+    double* const Wna = &sh.u.it.na[SIG<N>(hp ? k - 1 : N - 1)][ph];
+    double* const Wnb = &sh.u.it.nb[SIG<N>(hp ? k - 1 : N - 1)][hp ? (ph < 6 ? ph + 6 : ph - 6) : ph];
     double* const Wdump = &sh.dump[t];
     const int oB0 = FO<N>(k, 0, 0) + (ph >= 9 ? ph - 8 : 0);  // B row ph on force (fp, cp): + 24 fp + 7 cp
     auto launder_p = [&]() __attribute__((always_inline)) {
@@ -1420,11 +1437,13 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma nounroll
           for (int rep_ = 0; rep_ < MPCQ_REP_SWEEP; ++rep_) {  // > 1: timing experiments only
           double xp = 0.0;
-          // rows of step 1: G / H (half 0); S^{-1} of stage kk(-1), never stored (half 1).
-          // Iteration-invariant: wave 0 reads them before the barrier that publishes
-          // the right-hand sides, so their latency hides behind it.
-          lds_cd* Mp = half == 0 ? GHr + (GS * (cr == 0 ? 1 : N - 1) + RS * rr_)
-                                 : SmR + (GS * (cr == 0 ? -1 : N) + RS * rr_);
+          // Step-ordered bases (SIG): step j's rows / right-hand sides / w / X are at
+          // base + j * stride for every lane, an immediate offset.  Half 0: G_j (top,
+          // slot j) / H_{N-1-j} (bottom, slot MID+j); half 1: S^{-1} of stage kk(j-2),
+          // top slot j-2 / bottom slot MID-1+j.  Step 1's rows are iteration-invariant:
+          // wave 0 reads them before the barrier that publishes the right-hand sides.
+          lds_cd* const Mb = half == 0 ? GHr + (GS * (cr == 0 ? 0 : MID) + RS * rr_)
+                                       : SmR + (GS * (cr == 0 ? -2 : MID - 1) + RS * rr_);
           double g[12];
           auto row12 = [&](lds_cd* q) __attribute__((always_inline)) {  // 16-B aligned row: 6 ds_read_b128
 #pragma unroll
@@ -1434,7 +1453,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               g[2 * i + 1] = v.y;
             }
           };
-          if (t < 64) row12(Mp);
+          if (t < 64) row12(Mb + GS);
           sync_all();
           STAMP(3);
           if (t < 64) {
@@ -1442,43 +1461,51 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             // instance wait at the barrier): issue them ahead of a co-resident
             // instance's stage-parallel phases
             __builtin_amdgcn_s_setprio(3);
-            const int gs = cr == 0 ? GS : -GS, bs = cr == 0 ? 12 : -12;
-            lds_cd* BpN = (lds_cd*)&sh.u.it.bo[cr == 0 ? 0 : N - 1][rr_];  // bo; na, nb at +12N, +24N
-            lds_d* Yp = (lds_d*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? -1 : N) + rr_);  // w of kk(j-2)
+            // right-hand side of step j: top stage j (slot j), bottom stage N-1-j (slot
+            // MID+1+j, except the meeting stage MID at the bottom's last step MID-1, slot
+            // MID); na, nb at +12N, +24N
+            lds_cd* const Bb = (lds_cd*)&sh.u.it.bo[0][0] + (12 * (cr == 0 ? 0 : MID + 1) + rr_);
+            lds_cd* const Bm = (lds_cd*)&sh.u.it.bo[MID][rr_];
+            auto rhs = [&](int j) __attribute__((always_inline)) -> lds_cd* {  // j: a constant
+              return (j == MID - 1 && cr != 0) ? Bm : Bb + 12 * j;
+            };
+            // w of stage kk(j-2) (half 1): top slot j-2, bottom slot MID-1+j; the other
+            // lanes store into the sink with the same stride
+            lds_d* const sink = (lds_d*)&sh.red[0] + (t & 31);
+            lds_d* const Yb = (half == 1 && s < 12) ? (lds_d*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? -2 : MID - 1) + rr_)
+                                                    : sink;
             // right-hand sides run two steps ahead: step j sums the one of step j+1
             // (loaded during step j-1) and loads the one of step j+2; half 1 (the w
             // products) starts its chain from 0.  The first two (y_kk(0) and step 1's)
             // are loaded together and waited for once: they were published by the
             // barrier just passed, so this round trip is on the critical path.
             const double m0 = half == 0 ? 1.0 : 0.0;
-            double s0 = BpN[0], s1 = BpN[12 * N], s2 = BpN[24 * N];
-            double c0 = BpN[bs], c1 = BpN[bs + 12 * N], c2 = BpN[bs + 24 * N];
+            double s0 = rhs(0)[0], s1 = rhs(0)[12 * N], s2 = rhs(0)[24 * N];
+            double c0 = rhs(1)[0], c1 = rhs(1)[12 * N], c2 = rhs(1)[24 * N];
             asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(c0), "+v"(c1), "+v"(c2));
             double src = half == 0 ? (s0 + s1) + s2 : 0.0;  // y_kk(0) (half 0)
             double bcn = ((c0 + c1) + c2) * m0;
-            BpN += 2 * bs;
-            double b0 = BpN[0], b1 = BpN[12 * N], b2 = BpN[24 * N];
-            Mp += gs;
-            // first outward step: G_{MID}' (top) / H_{MID+1}' (bottom) columns
-            lds_cd* const MpO = GHr + (GS * (cr == 0 ? MID : MID + 1) + rr_);
-            BpN += bs;
+            double b0 = rhs(2)[0], b1 = rhs(2)[12 * N], b2 = rhs(2)[24 * N];
+            // outward step j reads G_{MID-j+1}' (top, slot MID+1-j) / H_{MID+j-1}'
+            // (bottom, slot N-j) columns: Ob + (MID - j) GS (LDS offsets are unsigned,
+            // so the bases sit at the lowest slot a chain reaches)
+            lds_cd* const Ob = GHr + (GS * (cr == 0 ? 1 : N - MID) + rr_);
 #pragma unroll
             for (int j = 1; j <= MID + 1; ++j) {
-              asm volatile("" : "+v"(Mp), "+v"(BpN), "+v"(Yp) : : "memory");
+              asm volatile("" : : : "memory");
               double gc[12];
 #pragma unroll
               for (int i = 0; i < 12; ++i) gc[i] = g[i];
               const double bc = j <= MID ? bcn : 0.0;
               if (j < MID) {  // prefetch the next step's rows
-                row12(Mp);
-                Mp += gs;
+                row12(Mb + GS * (j + 1));
               } else if (j == MID) {  // the meeting step: M^{-1} rows (half 0), the S walk (half 1)
-                row12(half == 0 ? GHr + RS * rr_ : Mp);
+                row12(half == 0 ? GHr + RS * rr_ : Mb + GS * (MID + 1));
                 lds_cd* qb = (lds_cd*)&sh.u.it.bo[MID][rr_];
                 b0 = qb[0]; b1 = qb[12 * N]; b2 = qb[24 * N];
               } else {  // the last step: the first outward step's columns
 #pragma unroll
-                for (int i = 0; i < 12; ++i) g[i] = MpO[RS * i];
+                for (int i = 0; i < 12; ++i) g[i] = Ob[RS * i + GS * (MID - 1)];
               }
               asm volatile("" : : : "memory");  // the prefetch is issued here, not sunk to its use
               double s_in = src;
@@ -1490,58 +1517,57 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               asm volatile("" : "+v"(b0), "+v"(b1), "+v"(b2));
               if (j < MID) bcn = ((b0 + b1) + b2) * m0;
               if (j + 2 <= MID) {
-                b0 = BpN[0]; b1 = BpN[12 * N]; b2 = BpN[24 * N];
-                BpN += bs;
+                b0 = rhs(j + 2)[0]; b1 = rhs(j + 2)[12 * N]; b2 = rhs(j + 2)[24 * N];
               }
-              if (j >= 2) {  // half 1: w of stage kk(j-2) (the meeting stage itself has none)
-                const bool wok = half == 1 && s < 12 && (j <= MID || cr == 0);
-                *(wok ? Yp : (lds_d*)&sh.dump[t]) = acc;
+              if (j >= 2 && j <= MID) {  // half 1: w of stage kk(j-2)
+                Yb[12 * j] = acc;
+              } else if (j == MID + 1) {  // the meeting stage itself has no w (bottom)
+                *(cr == 0 ? Yb + 12 * j : sink) = acc;
               }
-              Yp += bs;
               if (j <= MID) {
                 // half 0 continues with y_kk(j) (the bottom's step MID is idle), half 1
                 // receives y_kk(j-1) from half 0
-                const bool adv = cr == 0 || N - 1 - j >= MID;
+                const bool adv = j < MID || cr == 0;
                 src = keep_lo_take_lo(adv ? acc : src, src);
               } else {
                 xp = acc;
-                if (cr == 0 && half == 0 && s < 12) sh.u.it.xs[MID + 1][rr_] = xp;
+                if (cr == 0 && half == 0 && s < 12) sh.u.it.xs[SIGX<N>(MID + 1)][rr_] = xp;
               }
             }
             STAMP(6);
-            // Outward step j: top kk = MID-j: X_kk = w_kk - G_{kk+1}' X_{kk+1} (G_{kk+1} in
-            // GH[kk+1]); bottom kk = MID+j: X_kk = w_kk - H_{kk-1}' X_{kk-1} (H_{kk-1} in
-            // GH[kk]).  Lane rr reads column rr (a full 12-term product per lane; half 1
-            // repeats half 0).  The bottom row's last step (kk = N) is idle: its loads stay
-            // inside the shared memory block and its store goes to the lane's sink.
-            const int ms = cr == 0 ? -GS : GS, ws = cr == 0 ? -12 : 12;
-            lds_cd* MpN = MpO;  // its first columns were read during the meeting step
-            lds_cd* WpN = (lds_cd*)&sh.u.it.yv[cr == 0 ? MID - 1 : MID + 1][rr_];
-            lds_d* Xp = (lds_d*)&sh.u.it.xs[cr == 0 ? MID : MID + 2][rr_];
-            MpN += ms;
+            // Outward step j: top kk = MID-j: X_kk = w_kk - G_{kk+1}' X_{kk+1}; bottom
+            // kk = MID+j: X_kk = w_kk - H_{kk-1}' X_{kk-1} (columns from Ob - j GS).  Lane
+            // rr reads column rr (a full 12-term product per lane; half 1 repeats half 0).
+            // w of stage kk: top slot MID-j, bottom slot N-j (Wb - 12 j); X_kk = xs[kk+1]:
+            // top slot MID+1-j, bottom slot N-j (SIGX; Xb - 12 j).  The bottom row's last
+            // step (kk = N) is idle: its store goes to the sink.
+            // (bases at step MID's slot: step j at base + 12 (MID - j))
+            lds_cd* const Wb = (lds_cd*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? 0 : N - MID) + rr_);
+            lds_d* const sinkO = (lds_d*)&sh.red[0] + (t & 31);
+            lds_d* const Xb = (half == 0 && s < 12) ? (lds_d*)&sh.u.it.xs[0][0] + (12 * (cr == 0 ? 1 : N - MID) + rr_)
+                                                    : sinkO;
             wave_sync();  // the w written by half 1
-            double bq = WpN[0];
-            WpN += ws;
+            double bq = Wb[12 * (MID - 1)];
 #pragma unroll
             for (int j = 1; j <= MID; ++j) {
-              asm volatile("" : "+v"(MpN), "+v"(WpN), "+v"(Xp) : : "memory");
+              asm volatile("" : : : "memory");
               double gc[12];
 #pragma unroll
               for (int i = 0; i < 12; ++i) gc[i] = g[i];
               const double bc = bq;
               if (j < MID) {
 #pragma unroll
-                for (int i = 0; i < 12; ++i) g[i] = MpN[RS * i];
-                MpN += ms;
-                bq = WpN[0];
-                WpN += ws;
+                for (int i = 0; i < 12; ++i) g[i] = Ob[RS * i + GS * (MID - j - 1)];
+                bq = Wb[12 * (MID - j - 1)];
               }
               asm volatile("" : : : "memory");
               const double acc = bdot12(gc, xp, bc);  // x = w - G' x_next with -G stored
-              const bool act = cr == 0 || MID + j <= N - 1;
-              xp = act ? acc : xp;
-              *(act && half == 0 && s < 12 ? Xp : (lds_d*)&sh.dump[t]) = acc;
-              Xp += ws;
+              if (j < MID) {
+                xp = acc;
+                Xb[12 * (MID - j)] = acc;
+              } else {
+                *(cr == 0 ? Xb : sinkO) = acc;
+              }
             }
             __builtin_amdgcn_s_setprio(0);
           }
@@ -1563,8 +1589,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           const double cFb = Ab[oFb], cFa = Ab[oFa], cF4 = Ab[oF4], cSw = Ab[oF + 4];
           sync_all();
           STAMP(7);
-          const double xa = XSr[oXSp], xb = XSr[oXSp6];
-          sX = XSr[oXS];
+          const double xa = XSr[rXSp], xb = XSr[rXSp6];
+          sX = XSr[rXS];
           asm volatile("" : : : "memory");
           {
             gv = eXd * sX + eHd * xa;  // used from the lanes of rows 6..11 only

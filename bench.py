@@ -412,11 +412,11 @@ def main():
     fl = model.flops(N, iters, info[:, 0], p.check_termination,
                      p.adaptive_rho_interval if p.adaptive_rho else 0, p.scaling,
                      polish_rounds=info[:, 2] if args.polish else None,
-                     polish_solves=1 + max(p.polish_refine_iter, 10)).sum()
+                     polish_solves=1 + max(p.polish_refine_iter, 20 if N > 32 else 10)).sum()
     fl_dense = model.flops(N, iters, info[:, 0], p.check_termination,
                            p.adaptive_rho_interval if p.adaptive_rho else 0, p.scaling,
                            polish_rounds=info[:, 2] if args.polish else None,
-                           polish_solves=1 + max(p.polish_refine_iter, 10), structured=False).sum()
+                           polish_solves=1 + max(p.polish_refine_iter, 20 if N > 32 else 10), structured=False).sum()
     by = model.bytes_per_instance(N) * per
 
     # after the timed region: one more launch that also returns x and y (the

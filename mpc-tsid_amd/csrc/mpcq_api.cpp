@@ -22,6 +22,8 @@ struct mpcq_ctx {
   hipStream_t stream = nullptr;
   void* arena = nullptr;
   size_t arena_bytes = 0;
+  void* work = nullptr;  // engine workspace (horizons beyond 32 stages)
+  size_t work_bytes = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool have_form = false, have_solve = false;
   uint64_t* stamps = nullptr;
@@ -101,6 +103,28 @@ int ensure_arena(mpcq_ctx* c, size_t bytes) {
     return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) failed", want);
   }
   c->arena_bytes = want;
+  return MPCQ_OK;
+}
+
+// The engine's per-instance workspace (mpcq::work_doubles(N), zero up to 32 stages).
+int ensure_work(mpcq_ctx* c, int64_t B, double** out) {
+  *out = nullptr;
+  const size_t bytes = (size_t)mpcq::work_doubles(c->N) * 8 * (size_t)B;
+  if (bytes == 0) return MPCQ_OK;
+  if (bytes > c->work_bytes) {
+    if (c->work) {
+      HIP_TRY(hipStreamSynchronize(c->stream));  // a queued launch may still use it
+      HIP_TRY(hipFree(c->work));
+    }
+    c->work = nullptr;
+    c->work_bytes = 0;
+    if (hipMalloc(&c->work, bytes) != hipSuccess) {
+      c->work = nullptr;
+      return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) for the engine workspace failed", bytes);
+    }
+    c->work_bytes = bytes;
+  }
+  *out = (double*)c->work;
   return MPCQ_OK;
 }
 
@@ -231,7 +255,7 @@ int mpcq_create(int device, int n_steps, const mpcq_params* params, mpcq_ctx** o
   if (!out) return fail(MPCQ_E_INVALID, "out is NULL");
   *out = nullptr;
   if (!mpcq::horizon_supported(n_steps))
-    return fail(MPCQ_E_UNSUPPORTED, "horizon N=%d not compiled in (supported: N = 4j, 4 <= N <= 32)", n_steps);
+    return fail(MPCQ_E_UNSUPPORTED, "horizon N=%d not compiled in (supported: N = 4j, 4 <= N <= 32, and 48)", n_steps);
   mpcq_params p;
   if (params) p = *params;
   else mpcq_default_params(&p);
@@ -265,6 +289,7 @@ int mpcq_destroy(mpcq_ctx* c) {
   DeviceGuard g(c->device);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   if (c->arena) (void)hipFree(c->arena);
+  if (c->work) (void)hipFree(c->work);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -378,6 +403,8 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
     a.info = info;
   }
   a.stamps = c->stamps;
+  rc = ensure_work(c, B, &a.work);
+  if (rc) return rc;
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   HIP_TRY(mpcq::launch_solve(N, fused, c->p, a, c->stream));
   HIP_TRY(hipEventRecord(c->ev[3], c->stream));
@@ -727,6 +754,10 @@ int mpcq_session_tick(mpcq_session* s, int k, const double* state, const double*
   la.rho_out = (double*)s->arr[MPCQ_SV_RHO];
   la.info = s->info;
   la.stamps = c->stamps;
+  {
+    const int wrc = ensure_work(c, B, &la.work);
+    if (wrc) return wrc;
+  }
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   HIP_TRY(mpcq::launch_solve(N, true, c->p, la, c->stream));
   HIP_TRY(hipEventRecord(c->ev[3], c->stream));

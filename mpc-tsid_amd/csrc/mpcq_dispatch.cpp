@@ -2,11 +2,13 @@
 // compiled once per horizon (Makefile: -DMPCQ_ENGINE_N=N); each unit exports
 // engine_launch_n<N>, and this file maps a context's N onto it.
 //
-// Horizons compiled in: every N = 4j up to 32.  One wave64 holds four 16-lane
-// stage rows, so N is a multiple of 4; the reference's n_steps = n_periods *
-// T_gait / dt (FootstepPlanner.py:55) gives N = 8, 16, 24, 32 for the usual
-// dt / n_periods.  N <= 16 fits two instances per CU, 20 <= N <= 32 one (LDS,
-// checked by static_asserts in mpcq_engine.hip).
+// Horizons compiled in: every N = 4j up to 32, and 48.  One wave64 holds four
+// 16-lane stage rows, so N is a multiple of 4; the reference's n_steps =
+// n_periods * T_gait / dt (FootstepPlanner.py:55) gives N = 8, 16, 24, 32, 48 for
+// the usual dt / n_periods.  N <= 16 fits two instances per CU, 20 <= N <= 32 one
+// (LDS, checked by static_asserts in mpcq_engine.hip); N = 48 keeps S^{-1}, F W
+// and R^{-1} Q in a per-instance global workspace (work_doubles, one instance per
+// CU).
 #include "mpcq_internal.h"
 
 namespace mpcq {

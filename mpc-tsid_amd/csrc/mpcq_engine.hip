@@ -249,8 +249,14 @@ __device__ __forceinline__ double wave_sum(double v) {
 template <typename P>
 __device__ __forceinline__ void lds_uniform(P*& q) {
   asm volatile("" : "+v"(q));
-  q = reinterpret_cast<P*>(static_cast<unsigned long>(
-      __builtin_amdgcn_readfirstlane(static_cast<int>(reinterpret_cast<unsigned long>(q)))));
+  if constexpr (sizeof(P*) == 4) {  // an LDS pointer
+    q = reinterpret_cast<P*>(static_cast<unsigned long>(
+        __builtin_amdgcn_readfirstlane(static_cast<int>(reinterpret_cast<unsigned long>(q)))));
+  } else {  // a global-workspace pointer (horizons beyond 32 stages)
+    const unsigned long long v = reinterpret_cast<unsigned long long>(q);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((int)v), hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+    q = reinterpret_cast<P*>(((unsigned long long)hi << 32) | lo);
+  }
 }
 // a wave-uniform double kept in SGPRs
 __device__ __forceinline__ double uni(double v) {
@@ -401,6 +407,18 @@ __device__ __forceinline__ double dyn_bound(const mpcq_params& p, const double* 
 // column read both touch distinct LDS banks.  GS = one stage's slot.
 constexpr int RS = 12, GS = 12 * RS;
 
+// Horizons beyond 32 stages do not fit a CU's LDS (N = 48: 236 KB): S^{-1}, F W and
+// R^{-1} Q move to a per-instance global workspace (LaunchArgs::work, work_doubles(N)
+// doubles per instance, L2-resident), the rest stays in LDS (N = 48: 140 KB).
+template <int N>
+constexpr bool kBig = N > 32;
+template <int N>
+struct Work {  // offsets (doubles) inside one instance's workspace
+  // two slots ahead of S^{-1}: the sweep's lagging half reads (and discards) the rows
+  // of slots -2 / -1 in its first steps, which in LDS fall on GH
+  static constexpr int SM = 2 * GS, FW = SM + N * GS, QL = FW + 72 * N, ZERO = QL + 36 * N, SIZE = ZERO + 72;
+};
+
 template <int N>
 struct Smem {
   double Ab[126 * N - 18];  // scaled constraint values, CSC order
@@ -410,9 +428,10 @@ struct Smem {
   // dynamics-row rho of stage k [108,120); during scaling the row factors; in
   // the prologue xref / fsteps / the gait walk.
   alignas(16) double GH[N][GS];
-  alignas(16) double Sm[N][GS];         // S_k^{-1} / U_k^{-1} of stage k at SIG(k), row-major (row stride RS)
-  double FWs[N][72];        // F_k W_k (12x6, row psi at [6 psi]); W_k = B_k' R on rows 6..11
-  double QL[N][36];         // B_k F_k W_k = R^{-1} W_k' F_k W_k (6x6)
+  // (N > 32: these three live in the global workspace, Work<N>)
+  alignas(16) double Sm[kBig<N> ? 1 : N][GS];  // S_k^{-1} / U_k^{-1} of stage k at SIG(k), row-major (row stride RS)
+  double FWs[kBig<N> ? 1 : N][72];  // F_k W_k (12x6, row psi at [6 psi]); W_k = B_k' R on rows 6..11
+  double QL[kBig<N> ? 1 : N][36];   // B_k F_k W_k = R^{-1} W_k' F_k W_k (6x6)
   union {
     struct {
       // sweep right-hand side of stage k's states = bo[k] + na[k] + nb[k]: bo from
@@ -463,9 +482,35 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
   STAMP_DECL
   lds_cd* Ab = (lds_cd*)sh.Ab;
   lds_cd* GHr = (lds_cd*)&sh.GH[0][0];
-  lds_cd* SmR = (lds_cd*)&sh.Sm[0][0];
-  lds_cd* FWr = (lds_cd*)&sh.FWs[0][0];
-  lds_cd* QLr = (lds_cd*)&sh.QL[0][0];
+  constexpr bool BIG = kBig<N>;
+  // S^{-1}, F W, R^{-1} Q: LDS, or (N > 32) this instance's global workspace
+  using wcd = std::conditional_t<BIG, const double, lds_cd>;
+  using wdd = std::conditional_t<BIG, double, lds_d>;
+  wcd* SmR;
+  wcd* FWr;
+  wcd* QLr;
+  wdd* SmW;
+  wdd* FWW;
+  wdd* QLW;
+  int zFW, zQL;  // offsets of a zero block from FWr / QLr (masked reads)
+  if constexpr (BIG) {
+    double* const wk = SOLVE ? a.work + b * Work<N>::SIZE : nullptr;  // (formulation only: unused)
+    SmW = wk + Work<N>::SM;
+    FWW = wk + Work<N>::FW;
+    QLW = wk + Work<N>::QL;
+    zFW = Work<N>::ZERO - Work<N>::FW;
+    zQL = Work<N>::ZERO - Work<N>::QL;
+    if (SOLVE && t < 72) wk[Work<N>::ZERO + t] = 0.0;
+  } else {
+    SmW = (wdd*)&sh.Sm[0][0];
+    FWW = (wdd*)&sh.FWs[0][0];
+    QLW = (wdd*)&sh.QL[0][0];
+    zFW = (int)(sh.zero - &sh.FWs[0][0]);
+    zQL = (int)(sh.zero - &sh.QL[0][0]);
+  }
+  SmR = (wcd*)SmW;
+  FWr = (wcd*)FWW;
+  QLr = (wcd*)QLW;
   double* const gh0 = &sh.GH[0][0];
   int fo = FO<N>(k, f, cc), xo = XO<N>(k, ph);  // own force / state column in Ab
   int cr = (t >> 4) & 1;            // sweep row (wave 0): 0 top-down, 1 bottom-up
@@ -856,7 +901,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         }
         if (cl) {
 #pragma unroll
-          for (int j = 0; j < 6; ++j) { gk[36 + 6 * ph + j] = fw[j]; sh.FWs[k][6 * ph + j] = fw[j]; }
+          for (int j = 0; j < 6; ++j) { gk[36 + 6 * ph + j] = fw[j]; FWW[72 * k + 6 * ph + j] = fw[j]; }
         }
         wave_sync();
         // Q = W' (F W): 36 entries over the row's 16 lanes
@@ -868,7 +913,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           for (int psi = 0; psi < 12; ++psi)
             acc += (r1 * Bc(k, 6 + j1, psi / 3, psi % 3)) * gk[36 + 6 * psi + j2];
           gk[e] = acc;
-          sh.QL[k][e] = acc / r1;
+          QLW[36 * k + e] = acc / r1;
         }
       }
       const double dgX = PbX() + sigma;
@@ -941,7 +986,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           gj12(Ro, ph, ok);
           if (cl) {
 #pragma unroll
-            for (int ci = 0; ci < 12; ++ci) sh.Sm[SIG<N>(k)][RS * ph + ci] = Ro[ci];
+            for (int ci = 0; ci < 12; ++ci) SmW[GS * SIG<N>(k) + RS * ph + ci] = Ro[ci];
           }
           wave_sync();  // the previous inverse has been consumed by this row
           if (cl) {
@@ -985,8 +1030,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     // terms beta, (R^-1 Q) g only on the velocity rows), so no selects are needed
     const int oHdm = hp ? oHd : (int)(sh.zero - sh.Ab);
     const int oH6m = hp && !isv ? oH6 : (int)(sh.zero - sh.Ab);
-    const int oFWcm = isv ? oFWc : (int)(sh.zero - &sh.FWs[0][0]);
-    const int oQLm = isv ? oQL : (int)(sh.zero - &sh.QL[0][0]);
+    const int oFWcm = isv ? oFWc : zFW;
+    const int oQLm = isv ? oQL : zQL;
     lds_cd* XSr = (lds_cd*)&sh.u.it.xs[0][0];
     double* const Wbo = &sh.u.it.bo[SIG<N>(k)][ph];
     double* const Wna = &sh.u.it.na[SIG<N>(hp ? k - 1 : N - 1)][ph];
@@ -1442,13 +1487,19 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           // slot j) / H_{N-1-j} (bottom, slot MID+j); half 1: S^{-1} of stage kk(j-2),
           // top slot j-2 / bottom slot MID-1+j.  Step 1's rows are iteration-invariant:
           // wave 0 reads them before the barrier that publishes the right-hand sides.
-          lds_cd* const Mb = half == 0 ? GHr + (GS * (cr == 0 ? 0 : MID) + RS * rr_)
-                                       : SmR + (GS * (cr == 0 ? -2 : MID - 1) + RS * rr_);
+          // (N > 32: S^{-1} is global, so the row pointer is a generic one)
+          using swp = std::conditional_t<BIG, const double, lds_cd>;
+          using swp2 = std::conditional_t<BIG, const dbl2, lds_cd2>;
+          swp* GHs;
+          if constexpr (BIG) GHs = (const double*)&sh.GH[0][0];
+          else GHs = GHr;
+          swp* const Mb = half == 0 ? GHs + (GS * (cr == 0 ? 0 : MID) + RS * rr_)
+                                    : (swp*)SmR + (GS * (cr == 0 ? -2 : MID - 1) + RS * rr_);
           double g[12];
-          auto row12 = [&](lds_cd* q) __attribute__((always_inline)) {  // 16-B aligned row: 6 ds_read_b128
+          auto row12 = [&](swp* q) __attribute__((always_inline)) {  // 16-B aligned row: 6 ds_read_b128
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-              const dbl2 v = ((lds_cd2*)q)[i];
+              const dbl2 v = ((swp2*)q)[i];
               g[2 * i] = v.x;
               g[2 * i + 1] = v.y;
             }
@@ -1500,7 +1551,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               if (j < MID) {  // prefetch the next step's rows
                 row12(Mb + GS * (j + 1));
               } else if (j == MID) {  // the meeting step: M^{-1} rows (half 0), the S walk (half 1)
-                row12(half == 0 ? GHr + RS * rr_ : Mb + GS * (MID + 1));
+                row12(half == 0 ? GHs + RS * rr_ : Mb + GS * (MID + 1));
                 lds_cd* qb = (lds_cd*)&sh.u.it.bo[MID][rr_];
                 b0 = qb[0]; b1 = qb[12 * N]; b2 = qb[24 * N];
               } else {  // the last step: the first outward step's columns
@@ -1749,7 +1800,10 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
                               (p.polish >= 2 && (status == MPCQ_STATUS_SOLVED_INACCURATE ||
                                                  status == MPCQ_STATUS_MAX_ITER_REACHED)))) {
           constexpr double kPolishRho = 1e3;
-          constexpr int kPolishMinIter = 10;
+          // the refinement contracts by the error of the explicit stage inverses, which
+          // grows with the chain length: 10 steps land within 2e-10 of x* up to N = 32,
+          // N = 48 needs 20 (measured: 10 -> 2-4e-7, 20 -> 1e-10, tools/polish48b.py)
+          constexpr int kPolishMinIter = N > 32 ? 20 : 10;
           const double a_pri = pri_res, a_dua = dua_res;
           const double axf = xf, axX = xX;
           double az[3], ay[3], zs[3], ys[3], bred[3], prho[3];
@@ -1946,6 +2000,7 @@ template <int N>
 hipError_t launch_t(bool fused, bool solve, const mpcq_params& p, const LaunchArgs& a,
                     hipStream_t s) {
   const dim3 grid((unsigned)a.batch), block(16 * N);
+  if (kBig<N> && solve && !a.work) return hipErrorInvalidValue;  // the caller sizes it with work_doubles(N)
   // polish lives in its own instantiation: the production kernel's code (and its
   // register allocation in the ADMM loop) does not carry it
   const bool pol = p.polish != 0;
@@ -1966,6 +2021,8 @@ hipError_t launch_t(bool fused, bool solve, const mpcq_params& p, const LaunchAr
 #endif
 static_assert(MPCQ_ENGINE_N % 4 == 0 && MPCQ_ENGINE_N >= 4, "a wave64 holds four 16-lane stage rows");
 static_assert(sizeof(Smem<MPCQ_ENGINE_N>) <= 160 * 1024, "Smem<N> exceeds the CU's LDS");
+static_assert(Work<MPCQ_ENGINE_N>::SIZE == (kBig<MPCQ_ENGINE_N> ? work_doubles(MPCQ_ENGINE_N) : 72 + Work<MPCQ_ENGINE_N>::ZERO),
+              "work_doubles(N) (mpcq_internal.h) and Work<N> disagree");
 static_assert(MPCQ_ENGINE_N > 16 || sizeof(Smem<MPCQ_ENGINE_N>) <= 80 * 1024,
               "Smem<N> must fit twice in a CU for N <= 16");
 

@@ -31,7 +31,13 @@ struct LaunchArgs {
   double* rho_out;     // [B]
   int32_t* info;       // [B][4]: rho updates, polish status, polish rounds, reserved
   uint64_t* stamps;    // [B][16] diagnostic build only (MPCQ_STAMPS): cycles per phase
+  double* work;        // [B][work_doubles(N)] engine workspace (N > 32 only, else unused)
 };
+
+// Doubles of engine workspace per instance: 0 up to 32 stages (everything in LDS);
+// beyond, a 288-double pad, S^{-1} (N x 144), F W (N x 72), R^{-1} Q (N x 36) and a
+// zero block (72)
+constexpr int64_t work_doubles(int N) { return N > 32 ? 288 + (int64_t)N * (144 + 72 + 36) + 72 : 0; }
 
 // Planner launch (mpcq_planner.hip); layouts in include/mpcq.h (mpcq_plan_batch).
 struct PlanArgs {
@@ -84,7 +90,7 @@ hipError_t launch_retrieve(int N, const SessionArgs& a, hipStream_t s);
 hipError_t launch_formulate(int N, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);
 hipError_t launch_solve(int N, bool fused, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);
 // the horizons the engine is compiled for (mpcq_dispatch.cpp, Makefile)
-#define MPCQ_HORIZONS(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32)
+#define MPCQ_HORIZONS(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(48)
 bool horizon_supported(int N);
 int supported_horizons(int32_t* out, int cap);
 

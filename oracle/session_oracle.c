@@ -52,6 +52,7 @@ void oracle_retrieve(const mpcq_params* p, int N, const double* x, const double*
                      const double* fsteps, const double* gait, const double* shoulders, int failed,
                      double* x_robot, double* q_w, double* cost, double* warm_x, double* next_state,
                      double* next_l_feet) {
+  if (N < 1 || N > 64) return;  /* the planner's horizons (N <= 63) */
   const int NP = N + 1, n = 24 * N;
   for (int r = 0; r < 12; ++r)
     for (int k = 0; k < N; ++k) x_robot[r * N + k] = x[12 * k + r] + xref[r * NP + k + 1];
@@ -61,7 +62,7 @@ void oracle_retrieve(const mpcq_params* p, int N, const double* x, const double*
     else v = x[12 * N + (e - 12 * N + 12) % (12 * N)];
     warm_x[e] = failed ? 0.0 : v;
   }
-  double c[24 * 32];
+  double c[24 * 64];  /* N <= 64 (checked above) */
   for (int e = 0; e < n; ++e) {
     const double w = e < 12 * N ? p->state_weights[e % 12] : p->force_weight;
     c[e] = (x[e] * w) * x[e];

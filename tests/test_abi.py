@@ -75,7 +75,7 @@ def test_dims_and_pattern(mpcq, N, golden16, golden32):
 
 
 def test_supported_horizons(mpcq):
-    assert mpcq.supported_horizons() == [4, 8, 12, 16, 20, 24, 28, 32]
+    assert mpcq.supported_horizons() == [4, 8, 12, 16, 20, 24, 28, 32, 48]
 
 
 @pytest.mark.parametrize("N", [4, 8, 12, 20, 24, 28, 48])

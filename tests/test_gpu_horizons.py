@@ -1,9 +1,9 @@
-"""GPU parity at every compiled horizon (N = 4j <= 32): formulation vs the
-reference fixtures, the OSQP solve vs the oracle (statuses and iteration counts
-equal on every instance, x within X_TOL), the fused path on a synthetic batch,
-polish on the certified optimum x* (sessions at N = 8 / 24: test_gpu_session.py).  N = 48 (three
-gait periods at dt = 0.02) is refused with MPCQ_E_UNSUPPORTED: its stage data
-exceeds one CU's LDS in this layout."""
+"""GPU parity at every compiled horizon (N = 4j <= 32, and 48 = three gait periods
+at dt = 0.02): formulation vs the reference fixtures, the OSQP solve vs the oracle
+(statuses and iteration counts equal on every instance, x within X_TOL), the fused
+path on a synthetic batch, polish on the certified optimum x* (sessions:
+test_gpu_session.py).  N = 48 runs the global-workspace layout (S^{-1}, F W,
+R^{-1} Q outside LDS); other horizons are refused with an error code."""
 import numpy as np
 import pytest
 
@@ -13,7 +13,7 @@ FORM_TOL = 1e-13
 X_TOL = 1e-9     # golden QPs (a few hundred iterations)
 F_TOL = 5e-8     # fused synthetic batches: longer horizons and up to 4000 iterations amplify
                  # rounding (observed 1.5e-9 at N = 20 with identical iteration counts)
-COMPILED = (4, 8, 12, 20, 24, 28)  # 16 / 32: test_gpu_parity.py
+COMPILED = (4, 8, 12, 20, 24, 28, 48)  # 16 / 32: test_gpu_parity.py
 
 
 @pytest.fixture(scope="module")
@@ -30,9 +30,9 @@ def _rel(a, b):
 
 
 def test_supported_horizons(mpcq):
-    assert mpcq.supported_horizons() == [4, 8, 12, 16, 20, 24, 28, 32]
+    assert mpcq.supported_horizons() == [4, 8, 12, 16, 20, 24, 28, 32, 48]
     with pytest.raises(mpcq.MpcqError):
-        mpcq.Engine(48)
+        mpcq.Engine(36)
     with pytest.raises(mpcq.MpcqError):
         mpcq.Engine(18)
 

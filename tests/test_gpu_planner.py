@@ -25,7 +25,7 @@ def mpcq():
 
 @pytest.fixture(scope="module")
 def engines(mpcq):
-    es = {N: mpcq.Engine(N) for N in (8, 16, 24, 32)}
+    es = {N: mpcq.Engine(N) for N in (8, 16, 24, 32, 48)}
     yield es
     for e in es.values():
         e.close()
@@ -53,7 +53,7 @@ def _close(a, b, tol=PLAN_TOL):
     return float(d.max(initial=0)), float((d == 0).mean())
 
 
-@pytest.mark.parametrize("N", [8, 16, 24, 32])
+@pytest.mark.parametrize("N", [8, 16, 24, 32, 48])
 def test_planner_vs_reference_fixtures(mpcq, engines, N):
     """Every scenario of planner_golden.npz runs as one instance of a batch,
     tick by tick as processing.py:81-131 drives the reference."""

@@ -66,7 +66,7 @@ def _compare(sess, ors, mpcq, k, agree, plan_tol=1e-15, x_rtol=0.0):
     return float(np.abs(f0 - np.stack([o.f0 for o in ors])).max()), it
 
 
-@pytest.mark.parametrize("N,dual_warm", [(8, 0), (16, 0), (16, 1), (24, 1), (32, 0)])
+@pytest.mark.parametrize("N,dual_warm", [(8, 0), (16, 0), (16, 1), (24, 1), (32, 0), (48, 1)])
 def test_session_host_inputs_vs_oracle(mpcq, N, dual_warm):
     """Measured states from the host each tick (the reference's interface), with
     either dual carry-over (dual_warm = 1: osqp's scaled workspace y)."""

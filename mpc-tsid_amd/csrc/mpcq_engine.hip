@@ -399,12 +399,15 @@ __device__ __forceinline__ double dyn_bound(const mpcq_params& p, const double* 
 }
 
 // ---------------------------------------------------------------------------
-// Shared memory of one instance (N=16: 40.4 KB -> 4 instances per CU;
-// N=32: 80.2 KB -> 2).
+// Shared memory of one instance (N=16: 78.6 KB -> 2 instances per CU; N=32:
+// 156.7 KB -> 1; N=48: 140 KB with S^{-1} / F W / R^{-1} Q in global memory).
 
-// The sweep matrices (G / H / M^{-1} in GH, S^{-1} in Sm) are 12 x 12 with a row
-// stride of 13 doubles (26 banks): a row read (12 lanes, consecutive rows) and a
-// column read both touch distinct LDS banks.  GS = one stage's slot.
+// The sweep matrices (G / H / M^{-1} in GH, S^{-1} in Sm) are 12 x 12, row-major
+// with a row stride of RS = 12 doubles (96 B).  Column reads (the outward sweep:
+// 12 lanes, consecutive doubles) are conflict-free; the inward sweep's b128 row
+// reads (lane r at 96 r) collide 2-3 ways inside a 16-lane group.  A 13-double
+// stride removes that but needs 3 KB more LDS than two instances per CU leave at
+// N = 16.  GS = one stage's slot.
 constexpr int RS = 12, GS = 12 * RS;
 
 // Horizons beyond 32 stages do not fit a CU's LDS (N = 48: 236 KB): S^{-1}, F W and

@@ -21,10 +21,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--N", type=int, default=16)
+    ap.add_argument("--copies", type=int, default=-1,
+                    help=">= 0: every instance a copy of this instance of the C2 batch (seed 2)")
     a = ap.parse_args()
     import torch
     import mpcq
-    b = mpcq.synth.make_batch(a.batch, a.N, gaits=("trot",), seed=2000)
+    if a.copies >= 0:  # identical instances: per-phase cost alone (256) vs co-resident (512)
+        src = mpcq.synth.make_batch(1024, a.N, gaits=("trot",), seed=2)
+        b = {k: np.ascontiguousarray(np.repeat(src[k][a.copies:a.copies + 1], a.batch, axis=0))
+             for k in ("xref", "fsteps")}
+    else:
+        b = mpcq.synth.make_batch(a.batch, a.N, gaits=("trot",), seed=2000)
     dev = torch.device("cuda", 0)
     xr = torch.from_numpy(b["xref"]).to(dev)
     fs = torch.from_numpy(b["fsteps"]).to(dev)

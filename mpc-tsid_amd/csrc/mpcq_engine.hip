@@ -1431,7 +1431,21 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       // runs the state sweeps (P5-P7), ph_recover the forces and A w on the own rows
       // (P8, P9's first half).  The ADMM loop calls them with admm = true (w = rho z - y,
       // xc = sigma x); polish with its own w and x terms.
-      auto ph_rhs = [&](bool admm, const double (&pw)[3], double xcf, double xcX, double& uf,
+      // the iteration-invariant LDS operands of ph_rhs (A_f column, F W column, the
+      // state column's dynamics coefficients)
+      struct RhsOps {
+        double cf[10], fwc[12], cXd, cHd, cH6;
+      };
+      auto load_rhs_ops = [&](RhsOps& o) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 10; ++i) o.cf[i] = Ab[oF + i];
+#pragma unroll
+        for (int psi = 0; psi < 12; ++psi) o.fwc[psi] = FWr[oFWcm + 6 * psi];
+        o.cXd = Ab[oXd];
+        o.cHd = Ab[oHdm];
+        o.cH6 = Ab[oH6m];
+      };
+      auto ph_rhs = [&](bool admm, const RhsOps& o, const double (&pw)[3], double xcf, double xcX, double& uf,
                         double& beta) __attribute__((always_inline)) {
           launder_p();
           // P1-P4: w = rho z - y; b_f = sigma x_f + A_f' w and u = F b_f, beta = R B u
@@ -1440,21 +1454,16 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           // columns (na, nb): the only LDS hand-off before the sweeps.
           // every LDS operand of this phase is iteration-invariant: issue all the loads
           // first (one LDS round trip instead of one per use)
-          double cf[10], fwc[12];
-#pragma unroll
-          for (int i = 0; i < 10; ++i) cf[i] = Ab[oF + i];
-#pragma unroll
-          for (int psi = 0; psi < 12; ++psi) fwc[psi] = FWr[oFWcm + 6 * psi];
-          const double cXd = Ab[oXd], cHd = Ab[oHdm], cH6 = Ab[oH6m];
+          const double cXd = o.cXd, cHd = o.cHd, cH6 = o.cH6;
           double w[3];
 #pragma unroll
           for (int j = 0; j < 3; ++j) w[j] = admm ? rr[j] * z[j] - y[j] : pw[j];
           // the phase's arithmetic starts after this point, the loads before it
           asm volatile("" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]) : : "memory");
-          const double bf = colF_c(cf, w) + (admm ? p.sigma * xf : xcf);  // b_f = sigma x_f + A_f' w (- q, q = 0)
+          const double bf = colF_c(o.cf, w) + (admm ? p.sigma * xf : xcf);  // b_f = sigma x_f + A_f' w (- q, q = 0)
           // u = F b_f (kept for the forces) and beta = R B u = (F W)' b_f (rows 6..11)
           uf = bdot_ln12(Fr, bf, 0.0);
-          beta = bdot_ln12(fwc, bf, 0.0);
+          beta = bdot_ln12(o.fwc, bf, 0.0);
           {
             const double wd = w[0] - beta;  // dynamics-row w less the force Schur term (beta = 0 on rows 0..5)
             const double bo = (admm ? p.sigma * xX : xcX) + cXd * wd;
@@ -1628,7 +1637,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           wave_sync();
           }  // MPCQ_REP_SWEEP
       };
-      auto ph_recover = [&](double uf, double beta, double& sf, double& sX, double (&ax)[3])
+      auto ph_recover = [&](const RhsOps& o, double uf, double beta, double& sf, double& sX, double (&ax)[3])
           __attribute__((always_inline)) {
           // P8: forces f_k = F_k (b_f - R B' g) = u - (F W) g, with g = Xd X_{k+1} + Hd X_k
           // on the velocity rows (the states' part of those rows)
@@ -1639,8 +1648,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           double fwl[6], qll[6];
 #pragma unroll
           for (int i = 0; i < 6; ++i) { fwl[i] = FWr[oFW + i]; qll[i] = QLr[oQLm + i]; }
-          const double eXd = Ab[oXd], eHd = Ab[oHdm], eH6 = Ab[oH6m];
-          const double cFb = Ab[oFb], cFa = Ab[oFa], cF4 = Ab[oF4], cSw = Ab[oF + 4];
+          const double eXd = o.cXd, eHd = o.cHd, eH6 = o.cH6;  // (the same coefficients as ph_rhs's)
+          const double cFb = Ab[oFb], cFa = Ab[oFa], cF4 = Ab[oF4], cSw = o.cf[4];
           sync_all();
           STAMP(7);
           const double xa = XSr[rXSp], xb = XSr[rXSp6];
@@ -1701,13 +1710,13 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         // their own without them, so the check / infeasibility code and its live values
         // sit outside the hot loop's register allocation (inside it, they cost 0.31 us
         // per iteration through spills on the sweep path, measured).
-        auto admm_iter = [&](auto delta_tag, double (&dyv)[3], double& dxf_, double& dxX_)
+        auto admm_iter = [&](auto delta_tag, const RhsOps& ops, double (&dyv)[3], double& dxf_, double& dxX_)
             __attribute__((always_inline)) {
           constexpr bool DELTA = decltype(delta_tag)::value;
           double uf, beta, sf, sX, ax[3];
-          ph_rhs(true, kNoW, 0.0, 0.0, uf, beta);
+          ph_rhs(true, ops, kNoW, 0.0, 0.0, uf, beta);
           ph_sweep();
-          ph_recover(uf, beta, sf, sX, ax);
+          ph_recover(ops, uf, beta, sf, sX, ax);
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
             const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
@@ -1733,9 +1742,13 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           if (chk_on && to_check < until) until = to_check;
           if (adp_on && to_adapt < until) until = to_adapt;
           double dyv[3], dxf_, dxX_;
+          // held in registers through the iterations up to the next check: no LDS traffic
+          // for them in the loop
+          RhsOps ops;
+          load_rhs_ops(ops);
 #pragma nounroll
-          for (int r_ = 1; r_ < until; ++r_, ++iter) admm_iter(std::false_type{}, dyv, dxf_, dxX_);
-          admm_iter(std::true_type{}, dyv, dxf_, dxX_);
+          for (int r_ = 1; r_ < until; ++r_, ++iter) admm_iter(std::false_type{}, ops, dyv, dxf_, dxX_);
+          admm_iter(std::true_type{}, ops, dyv, dxf_, dxX_);
           // iter % check_termination == 0 / iter % adaptive_rho_interval == 0, by countdown
           const bool can_check = chk_on && (to_check -= until) == 0;
           if (can_check) to_check = p.check_termination;
@@ -1869,9 +1882,11 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
                 yp[j] = act[j] ? y[j] : 0.0;
                 pw[j] = act[j] ? kPolishRho * bred[j] - yp[j] : 0.0;
               }
-              ph_rhs(false, pw, p.sigma * xf, p.sigma * xX, uf, beta);
+              RhsOps po;
+              load_rhs_ops(po);
+              ph_rhs(false, po, pw, p.sigma * xf, p.sigma * xX, uf, beta);
               ph_sweep();
-              ph_recover(uf, beta, xpf, xpX, ax);
+              ph_recover(po, uf, beta, xpf, xpX, ax);
 #pragma unroll
               for (int j = 0; j < 3; ++j) {
                 axp[j] = ax[j];
@@ -1885,9 +1900,11 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
                 ry[j] = act[j] ? bred[j] - axp[j] : 0.0;
                 pw[j] = act[j] ? kPolishRho * ry[j] - yp[j] : 0.0;
               }
-              ph_rhs(false, pw, -Pbf() * xpf, -PbX() * xpX, uf, beta);
+              RhsOps po;
+              load_rhs_ops(po);
+              ph_rhs(false, po, pw, -Pbf() * xpf, -PbX() * xpX, uf, beta);
               ph_sweep();
-              ph_recover(uf, beta, dxf, dxX, ax);
+              ph_recover(po, uf, beta, dxf, dxX, ax);
               xpf += dxf;
               xpX += dxX;
 #pragma unroll

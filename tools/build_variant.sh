@@ -14,7 +14,7 @@ for n in 16 32; do /opt/rocm/bin/hipcc $F "$@" -DMPCQ_ENGINE_N=$n -c -o $OUT/$NA
 wait
 # the other horizons from the production objects
 OBJS="$OUT/$NAME/e16.o $OUT/$NAME/e32.o"
-for n in 4 8 12 20 24 28; do OBJS="$OBJS $C/build/engine_n$n.o"; done
+for n in 4 8 12 20 24 28 48; do OBJS="$OBJS $C/build/engine_n$n.o"; done
 /opt/rocm/bin/hipcc $F -shared -o $OUT/libmpcq_$NAME.so $OBJS $C/build/mpcq_planner.o $C/build/mpcq_session.o \
   $C/build/mpcq_api.o $C/build/mpcq_dispatch.o
 echo "built $OUT/libmpcq_$NAME.so"

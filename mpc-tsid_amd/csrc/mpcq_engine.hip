@@ -452,7 +452,7 @@ struct Smem {
   // per-row partial reductions; during the sweeps the sink of lanes whose store is void
   double red[(12 * N > 12 * (N / 2 + 1) + 64) ? 12 * N : 12 * (N / 2 + 1) + 64];
   double dump[16 * N];      // per-lane sink: predicated stores write here instead of branching
-  double zero[72];          // zeros: masked coefficient reads point here instead of selecting
+  alignas(16) double zero[72];  // zeros: masked coefficient reads point here instead of selecting
   int flag[4];
 };
 
@@ -1647,7 +1647,12 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           // sweep's states after it
           double fwl[6], qll[6];
 #pragma unroll
-          for (int i = 0; i < 6; ++i) { fwl[i] = FWr[oFW + i]; qll[i] = QLr[oQLm + i]; }
+          for (int i = 0; i < 3; ++i) {  // 16-B aligned pairs: ds_read_b128 (twice ds_read2_b64's LDS rate)
+            using wcd2 = std::conditional_t<BIG, const dbl2, lds_cd2>;
+            const dbl2 fa = ((wcd2*)(FWr + oFW))[i], qa = ((wcd2*)(QLr + oQLm))[i];
+            fwl[2 * i] = fa.x; fwl[2 * i + 1] = fa.y;
+            qll[2 * i] = qa.x; qll[2 * i + 1] = qa.y;
+          }
           const double eXd = o.cXd, eHd = o.cHd, eH6 = o.cH6;  // (the same coefficients as ph_rhs's)
           const double cFb = Ab[oFb], cFa = Ab[oFa], cF4 = Ab[oF4], cSw = o.cf[4];
           sync_all();

@@ -409,6 +409,15 @@ __device__ __forceinline__ double dyn_bound(const mpcq_params& p, const double* 
 // stride removes that but needs 3 KB more LDS than two instances per CU leave at
 // N = 16.  GS = one stage's slot.
 constexpr int RS = 12, GS = 12 * RS;
+// Offset of slot q in GH / Sm: the slots of the bottom chain (q > N/2) sit two
+// doubles (16 B) further on.  The sweep's b128 row reads put 4 lanes of one chain
+// and 8 of the other in each 16-lane bank group; rows 96 B apart cover only the
+// eight 4-bank slots at multiples of 8 dwords, so without the shift the two
+// chains' rows met in the same banks (2-way conflicts), with it they interleave.
+template <int N>
+constexpr int kSlotPad = 2;
+template <int N>
+__host__ __device__ constexpr int SLOT(int q) { return GS * q + (q > N / 2 ? kSlotPad<N> : 0); }
 
 // Horizons beyond 32 stages do not fit a CU's LDS (N = 48: 236 KB): S^{-1}, F W and
 // R^{-1} Q move to a per-instance global workspace (LaunchArgs::work, work_doubles(N)
@@ -419,7 +428,7 @@ template <int N>
 struct Work {  // offsets (doubles) inside one instance's workspace
   // two slots ahead of S^{-1}: the sweep's lagging half reads (and discards) the rows
   // of slots -2 / -1 in its first steps, which in LDS fall on GH
-  static constexpr int SM = 2 * GS, FW = SM + N * GS, QL = FW + 72 * N, ZERO = QL + 36 * N, SIZE = ZERO + 72;
+  static constexpr int SM = 2 * GS, FW = SM + N * GS + 2, QL = FW + 72 * N, ZERO = QL + 36 * N, SIZE = ZERO + 72;
 };
 
 template <int N>
@@ -431,8 +440,10 @@ struct Smem {
   // dynamics-row rho of stage k [108,120); during scaling the row factors; in
   // the prologue xref / fsteps / the gait walk.
   alignas(16) double GH[N][GS];
+  double GHpad[2];  // the bottom slots' shift (SLOT)
   // (N > 32: these three live in the global workspace, Work<N>)
-  alignas(16) double Sm[kBig<N> ? 1 : N][GS];  // S_k^{-1} / U_k^{-1} of stage k at SIG(k), row-major (row stride RS)
+  alignas(16) double Sm[kBig<N> ? 1 : N][GS];  // S_k^{-1} / U_k^{-1} of stage k at SLOT(SIG(k)), row-major (row stride RS)
+  double Smpad[2];
   double FWs[kBig<N> ? 1 : N][72];  // F_k W_k (12x6, row psi at [6 psi]); W_k = B_k' R on rows 6..11
   double QL[kBig<N> ? 1 : N][36];   // B_k F_k W_k = R^{-1} W_k' F_k W_k (6x6)
   union {
@@ -517,7 +528,10 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
   double* const gh0 = &sh.GH[0][0];
   int fo = FO<N>(k, f, cc), xo = XO<N>(k, ph);  // own force / state column in Ab
   int cr = (t >> 4) & 1;            // sweep row (wave 0): 0 top-down, 1 bottom-up
-  int rr_ = s < 12 ? s : 11;        // sweep lane's state index
+  // sweep lane's state index; lanes 12..15 (no state) repeat lanes 0..3, which sit in
+  // their bank group, so their reads broadcast instead of conflicting (measured:
+  // -2 % per iteration at N <= 16; +2 % at N = 32, which keeps lane 11's)
+  int rr_ = s < 12 ? s : (N <= 16 ? s - 12 : 11);
   // store v at q when c holds, else into this lane's sink (branch-free)
   auto launder = [&]() __attribute__((always_inline)) {
     lds_uniform(Ab); lds_uniform(GHr); lds_uniform(SmR); lds_uniform(FWr); lds_uniform(QLr);
@@ -784,6 +798,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 
     // ---- factorisation --------------------------------------------------------
     // dynamics-row rho of stage kk (published in GH[kk][108..120) at factor time)
+    // (stage-keyed scratch: unshifted slots; every read of it precedes the serial
+    // steps that overwrite the slots with G / H at SLOT offsets)
     auto rdy = [&](int kk, int i) __attribute__((always_inline)) { return GHr[GS * kk + 108 + i]; };
     auto Qv = [&](int kk, int j1, int j2) __attribute__((always_inline)) { return GHr[GS * kk + 6 * j1 + j2]; };
     // The factorisation's row builders are branch-free: every load is unconditional
@@ -852,7 +868,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       auto rho_of = [&](int j) __attribute__((always_inline)) -> double {
         return pr ? pr[j] : rho_of_cls(j);
       };
-      double* gk = sh.GH[k];
+      double* gk = gh0 + GS * k;
       if (cl) gk[108 + ph] = rho_of(0);
       sync_all();
       // ---- phase P: F_k = K_ff^{-1} (row ph per column lane), F_k W_k, Q_k
@@ -966,7 +982,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           asm volatile("" ::: "memory");
         }
         if (cl) {
-          double* const Gd = &sh.GH[upper ? SIG<N>(k) : SIG<N>(k + 1)][RS * ph];
+          double* const Gd = gh0 + SLOT<N>(upper ? SIG<N>(k) : SIG<N>(k + 1)) + RS * ph;
 #pragma unroll
           for (int ci = 0; ci < 12; ++ci) Gd[ci] = -G[ci];  // stored negated
         }
@@ -989,7 +1005,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           gj12(Ro, ph, ok);
           if (cl) {
 #pragma unroll
-            for (int ci = 0; ci < 12; ++ci) SmW[GS * SIG<N>(k) + RS * ph + ci] = Ro[ci];
+            for (int ci = 0; ci < 12; ++ci) SmW[SLOT<N>(SIG<N>(k)) + RS * ph + ci] = Ro[ci];
           }
           wave_sync();  // the previous inverse has been consumed by this row
           if (cl) {
@@ -1505,8 +1521,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           swp* GHs;
           if constexpr (BIG) GHs = (const double*)&sh.GH[0][0];
           else GHs = GHr;
-          swp* const Mb = half == 0 ? GHs + (GS * (cr == 0 ? 0 : MID) + RS * rr_)
-                                    : (swp*)SmR + (GS * (cr == 0 ? -2 : MID - 1) + RS * rr_);
+          // (the bottom chain's slots are past N/2: +2, SLOT)
+          swp* const Mb = half == 0 ? GHs + (GS * (cr == 0 ? 0 : MID) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_)
+                                    : (swp*)SmR + (GS * (cr == 0 ? -2 : MID - 1) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_);
           double g[12];
           auto row12 = [&](swp* q) __attribute__((always_inline)) {  // 16-B aligned row: 6 ds_read_b128
 #pragma unroll
@@ -1552,7 +1569,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             // outward step j reads G_{MID-j+1}' (top, slot MID+1-j) / H_{MID+j-1}'
             // (bottom, slot N-j) columns: Ob + (MID - j) GS (LDS offsets are unsigned,
             // so the bases sit at the lowest slot a chain reaches)
-            lds_cd* const Ob = GHr + (GS * (cr == 0 ? 1 : N - MID) + rr_);
+            lds_cd* const Ob = GHr + (GS * (cr == 0 ? 1 : N - MID) + (cr == 0 ? 0 : kSlotPad<N>) + rr_);
 #pragma unroll
             for (int j = 1; j <= MID + 1; ++j) {
               asm volatile("" : : : "memory");

@@ -35,9 +35,9 @@ struct LaunchArgs {
 };
 
 // Doubles of engine workspace per instance: 0 up to 32 stages (everything in LDS);
-// beyond, a 288-double pad, S^{-1} (N x 144), F W (N x 72), R^{-1} Q (N x 36) and a
-// zero block (72)
-constexpr int64_t work_doubles(int N) { return N > 32 ? 288 + (int64_t)N * (144 + 72 + 36) + 72 : 0; }
+// beyond, a 288-double pad, S^{-1} (N x 144 + 2), F W (N x 72), R^{-1} Q (N x 36)
+// and a zero block (72)
+constexpr int64_t work_doubles(int N) { return N > 32 ? 288 + (int64_t)N * (144 + 72 + 36) + 2 + 72 : 0; }
 
 // Planner launch (mpcq_planner.hip); layouts in include/mpcq.h (mpcq_plan_batch).
 struct PlanArgs {

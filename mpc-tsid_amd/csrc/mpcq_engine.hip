@@ -1461,9 +1461,14 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         o.cHd = Ab[oHdm];
         o.cH6 = Ab[oH6m];
       };
-      auto ph_rhs = [&](bool admm, const RhsOps& o, const double (&pw)[3], double xcf, double xcX, double& uf,
+      // o: the operands held in registers (the ADMM loop), or null: read them here (polish,
+      // whose loop would otherwise spill them)
+      auto ph_rhs = [&](bool admm, const RhsOps* op, const double (&pw)[3], double xcf, double xcX, double& uf,
                         double& beta) __attribute__((always_inline)) {
           launder_p();
+          RhsOps own_;
+          if (!op) load_rhs_ops(own_);
+          const RhsOps& o = op ? *op : own_;
           // P1-P4: w = rho z - y; b_f = sigma x_f + A_f' w and u = F b_f, beta = R B u
           // (stage-local, DPP only); then the sweep right-hand side of the own state
           // column (bo) and this stage's dynamics-row terms of stage k-1's state
@@ -1654,7 +1659,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           wave_sync();
           }  // MPCQ_REP_SWEEP
       };
-      auto ph_recover = [&](const RhsOps& o, double uf, double beta, double& sf, double& sX, double (&ax)[3])
+      auto ph_recover = [&](const RhsOps* op, double uf, double beta, double& sf, double& sX, double (&ax)[3])
           __attribute__((always_inline)) {
           // P8: forces f_k = F_k (b_f - R B' g) = u - (F W) g, with g = Xd X_{k+1} + Hd X_k
           // on the velocity rows (the states' part of those rows)
@@ -1670,8 +1675,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             fwl[2 * i] = fa.x; fwl[2 * i + 1] = fa.y;
             qll[2 * i] = qa.x; qll[2 * i + 1] = qa.y;
           }
-          const double eXd = o.cXd, eHd = o.cHd, eH6 = o.cH6;  // (the same coefficients as ph_rhs's)
-          const double cFb = Ab[oFb], cFa = Ab[oFa], cF4 = Ab[oF4], cSw = o.cf[4];
+          // (the same coefficients as ph_rhs's, from the held set when there is one)
+          const double eXd = op ? op->cXd : Ab[oXd], eHd = op ? op->cHd : Ab[oHdm], eH6 = op ? op->cH6 : Ab[oH6m];
+          const double cFb = Ab[oFb], cFa = Ab[oFa], cF4 = Ab[oF4], cSw = op ? op->cf[4] : Ab[oF + 4];
           sync_all();
           STAMP(7);
           const double xa = XSr[rXSp], xb = XSr[rXSp6];
@@ -1736,9 +1742,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             __attribute__((always_inline)) {
           constexpr bool DELTA = decltype(delta_tag)::value;
           double uf, beta, sf, sX, ax[3];
-          ph_rhs(true, ops, kNoW, 0.0, 0.0, uf, beta);
+          ph_rhs(true, &ops, kNoW, 0.0, 0.0, uf, beta);
           ph_sweep();
-          ph_recover(ops, uf, beta, sf, sX, ax);
+          ph_recover(&ops, uf, beta, sf, sX, ax);
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
             const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
@@ -1904,11 +1910,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
                 yp[j] = act[j] ? y[j] : 0.0;
                 pw[j] = act[j] ? kPolishRho * bred[j] - yp[j] : 0.0;
               }
-              RhsOps po;
-              load_rhs_ops(po);
-              ph_rhs(false, po, pw, p.sigma * xf, p.sigma * xX, uf, beta);
+              ph_rhs(false, nullptr, pw, p.sigma * xf, p.sigma * xX, uf, beta);
               ph_sweep();
-              ph_recover(po, uf, beta, xpf, xpX, ax);
+              ph_recover(nullptr, uf, beta, xpf, xpX, ax);
 #pragma unroll
               for (int j = 0; j < 3; ++j) {
                 axp[j] = ax[j];
@@ -1922,11 +1926,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
                 ry[j] = act[j] ? bred[j] - axp[j] : 0.0;
                 pw[j] = act[j] ? kPolishRho * ry[j] - yp[j] : 0.0;
               }
-              RhsOps po;
-              load_rhs_ops(po);
-              ph_rhs(false, po, pw, -Pbf() * xpf, -PbX() * xpX, uf, beta);
+              ph_rhs(false, nullptr, pw, -Pbf() * xpf, -PbX() * xpX, uf, beta);
               ph_sweep();
-              ph_recover(po, uf, beta, dxf, dxX, ax);
+              ph_recover(nullptr, uf, beta, dxf, dxX, ax);
               xpf += dxf;
               xpX += dxX;
 #pragma unroll

@@ -2,19 +2,23 @@
 # Build an experiment variant of the engine for timing (tools/iterbench.py):
 #   bash tools/build_variant.sh <name> <engine source> [extra hipcc flags]
 # -> mpc-tsid_amd/csrc/build/variants/libmpcq_<name>.so (loaded with
-#    MPCQ_LIB_VARIANT=exp:<name>); horizons 16 and 32 only, the rest of the
-#    library from the current objects (run make first).
+#    MPCQ_LIB_VARIANT=exp:<name>); horizons $VARIANT_HORIZONS (default 16 32) from
+#    the variant source, the rest of the library from the current objects (run
+#    make first).
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 C=$R/mpc-tsid_amd/csrc
 NAME=$1; SRC=$(realpath "$2"); shift 2
 OUT=$C/build/variants; mkdir -p $OUT/$NAME
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -I$C"
-for n in 16 32; do /opt/rocm/bin/hipcc $F "$@" -DMPCQ_ENGINE_N=$n -c -o $OUT/$NAME/e$n.o -x hip $SRC & done
+HS=${VARIANT_HORIZONS:-16 32}  # the horizons compiled from the variant source
+for n in $HS; do /opt/rocm/bin/hipcc $F "$@" -DMPCQ_ENGINE_N=$n -c -o $OUT/$NAME/e$n.o -x hip $SRC & done
 wait
 # the other horizons from the production objects
-OBJS="$OUT/$NAME/e16.o $OUT/$NAME/e32.o"
-for n in 4 8 12 20 24 28 48; do OBJS="$OBJS $C/build/engine_n$n.o"; done
+OBJS=""
+for n in 4 8 12 16 20 24 28 32 48; do
+  if [[ " $HS " == *" $n "* ]]; then OBJS="$OBJS $OUT/$NAME/e$n.o"; else OBJS="$OBJS $C/build/engine_n$n.o"; fi
+done
 /opt/rocm/bin/hipcc $F -shared -o $OUT/libmpcq_$NAME.so $OBJS $C/build/mpcq_planner.o $C/build/mpcq_session.o \
   $C/build/mpcq_api.o $C/build/mpcq_dispatch.o
 echo "built $OUT/libmpcq_$NAME.so"

@@ -1142,7 +1142,13 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         const bool uinf = hi_of(j) > kInf * kMinScaling, linf = lo_of(j) < -kInf * kMinScaling;
         dyp[j] = uinf ? (linf ? 0.0 : fmin(dy[j], 0.0)) : (linf ? fmax(dy[j], 0.0) : dy[j]);
       }
-      if (cl) { sh.u.it.na[k][ph] = dxX; sh.u.it.nb[k][ph] = dyp[0]; }
+      // published together with update_info's states / duals, one barrier for both
+      if (cl) {
+        sh.u.it.na[k][ph] = dxX;
+        sh.u.it.nb[k][ph] = dyp[0];
+        sh.u.it.yv[k][ph] = xX;
+        sh.u.it.bo[k][ph] = y[0];
+      }
       sync_all();
       launder_p();
       double ndy = 0.0, vu = -INFINITY, vl = -INFINITY, ineq = 0.0;
@@ -1198,10 +1204,13 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     // of each row then owns residual quantity s, reduced over the wave's rows by
     // permlane swaps and over the waves through red[].  INF: also combine the
     // partials of infeas_pass.
+    // INF: after infeas_pass, which has published the states / duals with its deltas
     auto update_info = [&](auto inf_tag) __attribute__((always_inline)) {
       constexpr bool INF = decltype(inf_tag)::value;
-      if (cl) { sh.u.it.yv[k][ph] = xX; sh.u.it.bo[k][ph] = y[0]; }
-      sync_all();
+      if constexpr (!INF) {
+        if (cl) { sh.u.it.yv[k][ph] = xX; sh.u.it.bo[k][ph] = y[0]; }
+        sync_all();
+      }
       STAMP(4);
       launder_p();
       lds_cd* const YV = (lds_cd*)&sh.u.it.yv[0][0];  // X_{k'} of stage k' >= 1 at 12 (k' - 1)

@@ -448,8 +448,9 @@ struct Smem {
   double QL[kBig<N> ? 1 : N][36];   // B_k F_k W_k = R^{-1} W_k' F_k W_k (6x6)
   union {
     struct {
-      // sweep right-hand side of stage k's states = bo[k] + na[k] + nb[k]: bo from
-      // stage k itself, na / nb from stage k+1's dynamics rows (Hd (w - beta), H6 w)
+      // sweep right-hand side of stage k's states = bo[k] + na[k]: bo from stage k
+      // itself, na from stage k+1's dynamics rows (Hd (w - beta) + H6 w, summed by
+      // ph_rhs); nb is scratch of the checks
       double bo[N][12];
       double na[N][12];
       double nb[N][12];
@@ -1054,7 +1055,6 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     lds_cd* XSr = (lds_cd*)&sh.u.it.xs[0][0];
     double* const Wbo = &sh.u.it.bo[SIG<N>(k)][ph];
     double* const Wna = &sh.u.it.na[SIG<N>(hp ? k - 1 : N - 1)][ph];
-    double* const Wnb = &sh.u.it.nb[SIG<N>(hp ? k - 1 : N - 1)][hp ? (ph < 6 ? ph + 6 : ph - 6) : ph];
     double* const Wdump = &sh.dump[t];
     const int oB0 = FO<N>(k, 0, 0) + (ph >= 9 ? ph - 8 : 0);  // B row ph on force (fp, cp): + 24 fp + 7 cp
     auto launder_p = [&]() __attribute__((always_inline)) {
@@ -1502,8 +1502,11 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             // stage 0 zeroes the last stage's na / nb (that stage has no next stage:
             // its coefficients read zero)
             *(cl ? Wbo : Wdump) = bo;
-            *(cl ? Wna : Wdump) = na;
-            *(cl ? Wnb : Wdump) = nb;
+            // stage k-1's component r takes na of lane r and nb of the lane 8 away in the
+            // row (component r -+ 6, LN): summed here, one value and one add less per
+            // sweep step
+            const double nbx = dppd<0x128>(nb);  // row_ror:8
+            *(cl ? Wna : Wdump) = na + nbx;
           }
           // (the barrier that publishes bo / na / nb opens ph_sweep)
       };
@@ -1574,12 +1577,12 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             // are loaded together and waited for once: they were published by the
             // barrier just passed, so this round trip is on the critical path.
             const double m0 = half == 0 ? 1.0 : 0.0;
-            double s0 = rhs(0)[0], s1 = rhs(0)[12 * N], s2 = rhs(0)[24 * N];
-            double c0 = rhs(1)[0], c1 = rhs(1)[12 * N], c2 = rhs(1)[24 * N];
-            asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(c0), "+v"(c1), "+v"(c2));
-            double src = half == 0 ? (s0 + s1) + s2 : 0.0;  // y_kk(0) (half 0)
-            double bcn = ((c0 + c1) + c2) * m0;
-            double b0 = rhs(2)[0], b1 = rhs(2)[12 * N], b2 = rhs(2)[24 * N];
+            double s0 = rhs(0)[0], s1 = rhs(0)[12 * N];
+            double c0 = rhs(1)[0], c1 = rhs(1)[12 * N];
+            asm volatile("" : "+v"(s0), "+v"(s1), "+v"(c0), "+v"(c1));
+            double src = half == 0 ? s0 + s1 : 0.0;  // y_kk(0) (half 0)
+            double bcn = (c0 + c1) * m0;
+            double b0 = rhs(2)[0], b1 = rhs(2)[12 * N];
             // outward step j reads G_{MID-j+1}' (top, slot MID+1-j) / H_{MID+j-1}'
             // (bottom, slot N-j) columns: Ob + (MID - j) GS (LDS offsets are unsigned,
             // so the bases sit at the lowest slot a chain reaches)
@@ -1596,22 +1599,22 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               } else if (j == MID) {  // the meeting step: M^{-1} rows (half 0), the S walk (half 1)
                 row12(half == 0 ? GHs + RS * rr_ : Mb + GS * (MID + 1));
                 lds_cd* qb = (lds_cd*)&sh.u.it.bo[MID][rr_];
-                b0 = qb[0]; b1 = qb[12 * N]; b2 = qb[24 * N];
+                b0 = qb[0]; b1 = qb[12 * N];
               } else {  // the last step: the first outward step's columns
 #pragma unroll
                 for (int i = 0; i < 12; ++i) g[i] = Ob[RS * i + GS * (MID - 1)];
               }
               asm volatile("" : : : "memory");  // the prefetch is issued here, not sunk to its use
               double s_in = src;
-              if (j == MID + 1) s_in = half == 0 ? row_pair_sum(src) - ((b0 + b1) + b2) : src;
+              if (j == MID + 1) s_in = half == 0 ? row_pair_sum(src) - (b0 + b1) : src;
               const double acc = bdot12(gc, s_in, bc);
               // the next right-hand side is summed after the chain: its loads were
               // issued at the end of the previous step, and summing them ahead of the
               // chain would put their LDS latency on the critical path
-              asm volatile("" : "+v"(b0), "+v"(b1), "+v"(b2));
-              if (j < MID) bcn = ((b0 + b1) + b2) * m0;
+              asm volatile("" : "+v"(b0), "+v"(b1));
+              if (j < MID) bcn = (b0 + b1) * m0;
               if (j + 2 <= MID) {
-                b0 = rhs(j + 2)[0]; b1 = rhs(j + 2)[12 * N]; b2 = rhs(j + 2)[24 * N];
+                b0 = rhs(j + 2)[0]; b1 = rhs(j + 2)[12 * N];
               }
               if (j >= 2 && j <= MID) {  // half 1: w of stage kk(j-2)
                 Yb[12 * j] = acc;

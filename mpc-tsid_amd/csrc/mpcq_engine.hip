@@ -593,7 +593,12 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
   double lo_g[FUSED ? 1 : 3], hi_g[FUSED ? 1 : 3];
   if (t == 0) { sh.flag[0] = 0; sh.flag[1] = 0; sh.flag[2] = 0; sh.flag[3] = 0; }
   for (int e = t; e < 72; e += T) sh.zero[e] = 0.0;  // N = 4: one wave of 64 lanes
-  if (t < 12) sh.u.it.xs[0][t] = 0.0;  // X_0 slot (masked reads multiply it by zero)
+  // The sweep arrays start at zero: a few lanes and steps read slots that are not
+  // (yet) written this launch — the bottom chain's idle last step, the lagging half's
+  // first rows — and discard the products or scale them by zero; LDS left over from
+  // an earlier workgroup can hold NaN / Inf, which a zero factor does not cancel.
+  // (X_0 slot xs[0] included: masked reads multiply it by zero.)
+  for (int e = t; e < (int)(sizeof(sh.u.it) / sizeof(double)); e += T) (&sh.u.it.bo[0][0])[e] = 0.0;
 
   // ---------------------------------------------------------------- prologue
   if (FUSED || !SOLVE) {

@@ -1,10 +1,12 @@
+# Every bench line of DESIGN.md §5 plus the rocprof passes, tagged: bash tools/bench_all.sh r02l
 set -o pipefail
+T=${1:?tag}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
-timeout -k 10 240 python -u bench.py > $O/r02j_bench_c2.json 2> $O/r02j_bench_c2.err &&
-timeout -k 10 240 python -u bench.py --no-polish > $O/r02j_bench_c2_nopolish.json 2> $O/r02j_bench_c2_nopolish.err &&
-timeout -k 10 240 python -u bench.py --config c3 > $O/r02j_bench_c3.json 2> $O/r02j_bench_c3.err &&
-timeout -k 10 240 python -u bench.py --config c1 > $O/r02j_bench_c1.json 2> $O/r02j_bench_c1.err &&
-timeout -k 10 300 python -u bench.py --config c4 --steps 3 --warmup 1 > $O/r02j_bench_c4_1gpu.json 2> $O/r02j_bench_c4.err &&
-timeout -k 10 300 python -u bench.py --config c5 --steps 3 --warmup 1 > $O/r02j_bench_c5_1gpu.json 2> $O/r02j_bench_c5.err &&
-bash tools/profile.sh r02j
+timeout -k 10 240 python -u bench.py > $O/${T}_bench_c2.json 2> $O/${T}_bench_c2.err &&
+timeout -k 10 240 python -u bench.py --no-polish > $O/${T}_bench_c2_nopolish.json 2> $O/${T}_bench_c2_nopolish.err &&
+timeout -k 10 240 python -u bench.py --config c3 > $O/${T}_bench_c3.json 2> $O/${T}_bench_c3.err &&
+timeout -k 10 240 python -u bench.py --config c1 > $O/${T}_bench_c1.json 2> $O/${T}_bench_c1.err &&
+timeout -k 10 300 python -u bench.py --config c4 --steps 3 --warmup 1 > $O/${T}_bench_c4_1gpu.json 2> $O/${T}_bench_c4.err &&
+timeout -k 10 300 python -u bench.py --config c5 --steps 3 --warmup 1 > $O/${T}_bench_c5_1gpu.json 2> $O/${T}_bench_c5.err &&
+bash tools/profile.sh $T

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile.sh run (gpurun_out/prof_<tag>) into profiles/.
 
-    python tools/prof_summary.py <tag> [--key c2_N16_B1024]
+    python tools/prof_summary.py <tag> [--key c2_N16_B1024_polish]
 
 Writes profiles/<tag>_kernel_stats.csv (the rocprofv3 --kernel-trace --stats
 summary), profiles/<tag>_summary.md (per-launch duration, HBM counters, SQ
@@ -43,7 +43,7 @@ def mean(v):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--key", default="c2_N16_B1024")
+    ap.add_argument("--key", default="c2_N16_B1024_polish")
     ap.add_argument("--instances", type=int, default=1024)
     ap.add_argument("--kernel", default="engine_kernel", help="substring of the kernel the counters describe")
     a = ap.parse_args()

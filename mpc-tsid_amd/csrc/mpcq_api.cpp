@@ -122,6 +122,9 @@ int ensure_work(mpcq_ctx* c, int64_t B, double** out) {
       c->work = nullptr;
       return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) for the engine workspace failed", bytes);
     }
+    // zeroed once: like the LDS sweep arrays, the padding slots the sweeps over-read
+    // must not hold NaN (a zero factor does not cancel it)
+    HIP_TRY(hipMemsetAsync(c->work, 0, bytes, c->stream));
     c->work_bytes = bytes;
   }
   *out = (double*)c->work;

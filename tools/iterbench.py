@@ -1,6 +1,6 @@
 """Per-iteration latency of the production kernel, free of the batch's tail effects.
 
-    python tools/iterbench.py [--N 16] [--reps 5]
+    python tools/iterbench.py [--N 16] [--reps 5] [--polish]
 
 Takes the C2 batch (bench.py's seeded synthetic instances), finds its slowest
 instance and launches B identical copies of it (B = 256: one instance per CU;
@@ -22,11 +22,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--N", type=int, default=16)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--pick", choices=("slowest", "fastest"), default="slowest",
+                    help="which instance of the batch to copy")
+    ap.add_argument("--polish", action="store_true", help="the bench's accuracy mode (polish=2 instantiation)")
     a = ap.parse_args()
     import torch
     import mpcq
     dev = torch.device("cuda", 0)
-    eng = mpcq.Engine(a.N)
+    eng = mpcq.Engine(a.N, **(dict(polish=2, polish_rounds=8, polish_refine_iter=10) if a.polish else {}))
     src = mpcq.synth.make_batch(1024, a.N, gaits=("trot",), seed=2)  # bench.py C2 data
 
     def run(xref, fsteps, reps):
@@ -44,9 +47,9 @@ def main():
         return it.cpu().numpy(), float(np.median(ms))
 
     its, ms = run(src["xref"], src["fsteps"], a.reps)
-    slow = int(np.argmax(its))
+    slow = int(np.argmax(its)) if a.pick == "slowest" else int(np.argmin(its))
     r = eng.solve(src["xref"][slow:slow + 1], src["fsteps"][slow:slow + 1])
-    print(f"C2 batch: kernel {ms:.3f} ms, iterations median {np.median(its):.0f} max {its.max()} (instance {slow}, "
+    print(f"C2 batch: kernel {ms:.3f} ms, iterations median {np.median(its):.0f} max {its.max()} ({a.pick}: instance {slow}, "
           f"{int(r['rho_updates'][0])} rho updates)")
     for B in (256, 512, 1024):
         xr = np.repeat(src["xref"][slow:slow + 1], B, axis=0)

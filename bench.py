@@ -97,20 +97,30 @@ def load_traffic(tag: str):
 
 
 def _dist_setup():
+    """One process per GPU (RANK / LOCAL_RANK / WORLD_SIZE from torch.distributed.run),
+    RCCL ("nccl") between them.  MPCQ_DIST_BACKEND=gloo is the rehearsal mode of the
+    N > 1 path on a box with fewer GPUs than ranks: ranks share devices round-robin
+    and the collectives (barriers, max-over-ranks, stats) run over gloo on the host."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("MPCQ_DIST_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        raise ValueError(f"MPCQ_DIST_BACKEND={backend!r}: 'nccl' (RCCL) or 'gloo'")
+    if backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(backend, init_method="env://")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    return torch, dist, world, rank, local, dev
+    coll = dev if backend == "nccl" else torch.device("cpu")  # where collective tensors live
+    return torch, dist, world, rank, local, dev, coll
 
 
-def _timed(torch, dist, dev, world, stream, step, steps, warmup):
+def _timed(torch, dist, dev, coll, world, stream, step, steps, warmup):
     """W untimed steps, then K steps between barriers + synchronisations; returns
     (max-over-ranks wall seconds, HIP-event ms per step on the launch stream)."""
     from mpcq import shard
@@ -133,13 +143,13 @@ def _timed(torch, dist, dev, world, stream, step, steps, warmup):
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    return shard.max_over_ranks(dist, wall, dev, world), ev0.elapsed_time(ev1) / max(steps, 1)
+    return shard.max_over_ranks(dist, wall, coll, world), ev0.elapsed_time(ev1) / max(steps, 1)
 
 
 def main_plan(args):
     """Batched FootstepPlanner (mpcq_plan_batch, MPCQ_PLAN_TICK) on device-resident
     robots: one step = one planner launch over this rank's robots."""
-    torch, dist, world, rank, local, dev = _dist_setup()
+    torch, dist, world, rank, local, dev, coll = _dist_setup()
     import mpcq
     from mpcq import model, synth
     N = CONFIGS[args.config]["N"]
@@ -166,7 +176,7 @@ def main_plan(args):
                         d["fsteps"].data_ptr(), status_ptr=d["status"].data_ptr(), reduced_ptr=d["red"].data_ptr(),
                         asynchronous=True)
 
-    wall, ms = _timed(torch, dist, dev, world, stream, step, args.steps, args.warmup)
+    wall, ms = _timed(torch, dist, dev, coll, world, stream, step, args.steps, args.warmup)
     ok = int((d["status"] == 0).sum().item())
     if rank == 0:
         by = model.planner_bytes_per_instance(N) * per
@@ -206,7 +216,7 @@ def main_plan(args):
 def main_tick(args):
     """Closed-loop sessions: one step = one tick of every robot on this rank
     (planner + warm-started fused solve + retrieve), virtual robot."""
-    torch, dist, world, rank, local, dev = _dist_setup()
+    torch, dist, world, rank, local, dev, coll = _dist_setup()
     import mpcq
     from mpcq import model, synth
     cfg = CONFIGS[args.config]
@@ -226,7 +236,7 @@ def main_tick(args):
     def step(i):
         sess.tick_device(vr.data_ptr(), k=i, asynchronous=True)
 
-    wall, ms = _timed(torch, dist, dev, world, stream, step, args.steps, warm)
+    wall, ms = _timed(torch, dist, dev, coll, world, stream, step, args.steps, warm)
     plan_ms, solve_ms = eng.last_kernel_ms()
     st = sess.read(mpcq.SV_STATUS)
     it = sess.read(mpcq.SV_ITERS)
@@ -322,17 +332,7 @@ def main():
         return main_plan(args)
     if args.mode == "tick":
         return main_tick(args)
-    import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    torch, dist, world, rank, local, dev, coll = _dist_setup()
 
     import mpcq
     from mpcq import model, shard
@@ -377,7 +377,7 @@ def main():
     def step():
         launch()
         if args.gather and world > 1:
-            shard.gather_rows(dist, f0_d, total, world, rank)  # forces of every instance on every rank
+            shard.gather_rows(dist, f0_d if coll.type == "cuda" else f0_d.cpu(), total, world, rank)  # forces of every instance on every rank
 
     torch.cuda.set_stream(stream)
     for _ in range(args.warmup):
@@ -400,7 +400,7 @@ def main():
     launch_ms = np.array([evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]) if args.steps else np.zeros(1)
     kern_ms = float(launch_ms.mean())
 
-    wall_max = shard.max_over_ranks(dist, wall, dev, world)
+    wall_max = shard.max_over_ranks(dist, wall, coll, world)
 
     status = st_d.cpu().numpy()
     iters = it_d.cpu().numpy()
@@ -434,7 +434,7 @@ def main():
         e2e.append(time.perf_counter() - t_)
     e2e_ms = float(np.median(e2e)) * 1e3
 
-    stats = torch.tensor([solved, per, fl, by, kern_ms], dtype=torch.float64, device=dev)
+    stats = torch.tensor([solved, per, fl, by, kern_ms], dtype=torch.float64, device=coll)
     if world > 1:
         allst = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(allst, stats)

@@ -258,7 +258,12 @@ int mpcq_session_destroy(mpcq_session* s);
  * v_ref [B][6], reduced [B] (NULL = 0); host pointers, or device pointers with
  * MPCQ_FLAG_DEVICE_PTRS.  state / l_feet NULL = the virtual robot (above).
  * k = MPC tick index (k == 0: first tick, MPC.py:491).  Blocking unless
- * MPCQ_FLAG_ASYNC together with MPCQ_FLAG_DEVICE_PTRS. */
+ * MPCQ_FLAG_ASYNC together with MPCQ_FLAG_DEVICE_PTRS.
+ * From the second tick on, the solve dispatches the robots longest-first by the
+ * previous tick's iteration counts (a fourth, one-workgroup launch after the
+ * retrieve builds the order); results do not depend on it.  The environment
+ * variable MPCQ_DISPATCH_ORDER=0, read at mpcq_session_create, keeps index order
+ * (timing comparisons only). */
 int mpcq_session_tick(mpcq_session* s, int k, const double* state, const double* l_feet,
                       const double* v_ref, const int32_t* reduced, uint32_t flags);
 

@@ -533,6 +533,9 @@ struct mpcq_session {
   double* in_lfeet = nullptr;
   double* in_vref = nullptr;
   int32_t* in_reduced = nullptr;
+  int32_t* order = nullptr;  // dispatch order of the next solve (longest previous first)
+  bool have_order = false;
+  bool use_order = true;  // MPCQ_DISPATCH_ORDER=0 turns it off (A/B timing only; results are identical)
 };
 
 namespace {
@@ -584,7 +587,7 @@ int mpcq_session_create(mpcq_ctx* c, int64_t B, const mpcq_planner_params* pp, c
   for (int w = 0; w < MPCQ_SV_COUNT; ++w) { s->bytes[w] = sv_bytes(w, B, N); off[w] = take(s->bytes[w]); }
   const size_t o_wx = take((size_t)B * 24 * N * 8), o_ps = take((size_t)B * 4), o_in = take((size_t)B * 16),
                o_st = take((size_t)B * 96), o_lf = take((size_t)B * 96), o_vr = take((size_t)B * 48),
-               o_rd = take((size_t)B * 4);
+               o_rd = take((size_t)B * 4), o_or = take((size_t)B * 4);
   DeviceGuard g(c->device);
   if (hipMalloc(&s->mem, tot) != hipSuccess) {
     delete s;
@@ -604,6 +607,11 @@ int mpcq_session_create(mpcq_ctx* c, int64_t B, const mpcq_planner_params* pp, c
   s->in_lfeet = (double*)(base + o_lf);
   s->in_vref = (double*)(base + o_vr);
   s->in_reduced = (int32_t*)(base + o_rd);
+  s->order = (int32_t*)(base + o_or);
+  {
+    const char* e = getenv("MPCQ_DISPATCH_ORDER");
+    s->use_order = !(e && e[0] == '0');
+  }
   // initial values: the reference objects' constructors
   const size_t hb = sv_bytes(MPCQ_SV_XREF, B, N) > sv_bytes(MPCQ_SV_FSTEPS, B, N) ? sv_bytes(MPCQ_SV_XREF, B, N)
                                                                                   : sv_bytes(MPCQ_SV_FSTEPS, B, N);
@@ -757,6 +765,9 @@ int mpcq_session_tick(mpcq_session* s, int k, const double* state, const double*
   la.rho_out = (double*)s->arr[MPCQ_SV_RHO];
   la.info = s->info;
   la.stamps = c->stamps;
+  // longest-first by the previous tick's iteration counts (a tick k == 0 restarts cold)
+  if (k == 0) s->have_order = false;
+  la.order = s->have_order && s->use_order ? s->order : nullptr;
   {
     const int wrc = ensure_work(c, B, &la.work);
     if (wrc) return wrc;
@@ -787,6 +798,8 @@ int mpcq_session_tick(mpcq_session* s, int k, const double* state, const double*
   ra.force_weight = c->p.force_weight;
   for (int i = 0; i < 8; ++i) ra.shoulders[i] = s->pp.shoulders[i];
   HIP_TRY(mpcq::launch_retrieve(N, ra, c->stream));
+  HIP_TRY(mpcq::launch_order((const int32_t*)s->arr[MPCQ_SV_ITERS], B, s->order, c->stream));
+  s->have_order = true;
   // host inputs are staged in buffers the next tick reuses: host calls block
   if (!(flags & MPCQ_FLAG_ASYNC) || !dev) HIP_TRY(hipStreamSynchronize(c->stream));
   return MPCQ_OK;

@@ -492,8 +492,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
   const bool cl = c < 3;          // column lane (c == 3: friction rows 3, 4 only)
   int cc = cl ? c : 2;            // column component; c == 3 shadows c == 2
   int ph = 3 * f + cc;            // own force / state index in the stage
-  const int64_t b = blockIdx.x;
-  if (b >= a.batch) return;
+  if ((int64_t)blockIdx.x >= a.batch) return;
+  const int64_t b = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;  // the instance
   STAMP_DECL
   lds_cd* Ab = (lds_cd*)sh.Ab;
   lds_cd* GHr = (lds_cd*)&sh.GH[0][0];

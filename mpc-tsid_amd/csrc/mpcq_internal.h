@@ -32,6 +32,7 @@ struct LaunchArgs {
   int32_t* info;       // [B][4]: rho updates, polish status, polish rounds, reserved
   uint64_t* stamps;    // [B][16] diagnostic build only (MPCQ_STAMPS): cycles per phase
   double* work;        // [B][work_doubles(N)] engine workspace (N > 32 only, else unused)
+  const int32_t* order; // [B] instance solved by workgroup i (a permutation of 0..B-1), or null: i
 };
 
 // Doubles of engine workspace per instance: 0 up to 32 stages (everything in LDS);
@@ -85,6 +86,9 @@ struct SessionArgs {
 };
 
 hipError_t launch_retrieve(int N, const SessionArgs& a, hipStream_t s);
+// Dispatch order of the next tick's solve (mpcq_session.hip): the robots sorted by
+// this tick's iteration counts, longest first (buckets of 16 iterations).
+hipError_t launch_order(const int32_t* iters, int64_t batch, int32_t* order, hipStream_t s);
 
 // Launchers (mpcq_engine.hip).  Return hipError_t.
 hipError_t launch_formulate(int N, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);

@@ -143,7 +143,42 @@ __global__ __launch_bounds__(64) void retrieve_kernel(SessionArgs a) {
   }
 }
 
+// Longest-first dispatch order from the iteration counts of the tick just solved
+// (one workgroup; counting sort over buckets of 16 iterations, LDS atomics, so the
+// order inside a bucket is arbitrary -- every instance's result is independent of
+// the workgroup that solves it).  A robot's warm-started count predicts its next
+// one (tools/tick_iters.py), and index-order dispatch puts long solves that land
+// late in the launch on its critical path.
+constexpr int kOrderBuckets = 256;
+__global__ __launch_bounds__(1024) void order_kernel(const int32_t* __restrict__ iters, int64_t B,
+                                                     int32_t* __restrict__ order) {
+  __shared__ int hist[kOrderBuckets];
+  const int t = threadIdx.x;
+  auto bucket = [](int32_t it) { const int q = (it > 0 ? it : 0) >> 4; return q < kOrderBuckets - 1 ? q : kOrderBuckets - 1; };
+  if (t < kOrderBuckets) hist[t] = 0;
+  __syncthreads();
+  for (int64_t i = t; i < B; i += blockDim.x) atomicAdd(&hist[bucket(iters[i])], 1);
+  __syncthreads();
+  if (t == 0) {  // exclusive offsets, the longest bucket first
+    int acc = 0;
+    for (int q = kOrderBuckets - 1; q >= 0; --q) {
+      const int h = hist[q];
+      hist[q] = acc;
+      acc += h;
+    }
+  }
+  __syncthreads();
+  for (int64_t i = t; i < B; i += blockDim.x) order[atomicAdd(&hist[bucket(iters[i])], 1)] = (int32_t)i;
+}
+
 }  // namespace
+
+hipError_t launch_order(const int32_t* iters, int64_t batch, int32_t* order, hipStream_t s) {
+  if (batch <= 0) return hipSuccess;
+  if (batch > INT32_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, s, iters, batch, order);
+  return hipGetLastError();
+}
 
 hipError_t launch_retrieve(int N, const SessionArgs& a, hipStream_t s) {
   if (a.batch <= 0) return hipSuccess;

@@ -179,3 +179,33 @@ def test_session_api_edges(mpcq):
         st = eng.plan(mpcq.PLAN_TICK, 0, z, np.zeros((0, 3, 4)), np.zeros((0, 6)), np.zeros((0, 20, 5)),
                       np.zeros(0, np.int32), np.zeros(0), np.zeros((0, 12, 17)), np.zeros((0, 20, 13)))
         assert st.shape == (0,)
+
+
+@pytest.mark.parametrize("N", [16, 32])
+def test_session_dispatch_order_changes_no_result(mpcq, monkeypatch, N):
+    """From the second tick on, a session dispatches its robots' solves longest-
+    previous-first (order_kernel, a permutation built on the device).  Every
+    robot's trajectory must be the same bit for bit as with index-order dispatch
+    (MPCQ_DISPATCH_ORDER=0): a lost or duplicated robot, or a workgroup reading
+    another robot's data, would show here.  600 robots: more workgroups than one
+    dispatch round at N = 32, so the order really moves work between rounds."""
+    B, T = 600, 6
+    gaits = _gaits(B, N)
+    rng = np.random.default_rng(9)
+    v_ref = np.stack([rng.uniform(-.4, .9, B), rng.uniform(-.2, .2, B), np.zeros(B), np.zeros(B), np.zeros(B),
+                      rng.uniform(-.5, .5, B)], axis=1)
+    names = ("SV_F0", "SV_X", "SV_Y", "SV_STATUS", "SV_ITERS", "SV_RHO", "SV_STATE", "SV_Q_W", "SV_COST")
+    runs = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MPCQ_DISPATCH_ORDER", flag)
+        out = []
+        with mpcq.Engine(N) as eng, mpcq.Session(eng, B, gait0=gaits) as sess:
+            for _ in range(T):
+                sess.tick(v_ref)
+                out.append({n: sess.read(getattr(mpcq, n)).copy() for n in names})
+        runs[flag] = out
+    iters = np.array([t["SV_ITERS"] for t in runs["1"]])
+    assert iters[1:].std() > 0  # the order is not the identity
+    for k in range(T):
+        for n in names:
+            assert np.array_equal(runs["0"][k][n], runs["1"][k][n], equal_nan=True), (k, n)

@@ -1131,17 +1131,23 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     };
     // OSQP 0.6's infeasibility tests (auxil.c is_primal_infeasible / is_dual_infeasible)
     // on the last iteration's delta_y (dy, own rows) and delta_x (dxf, dxX, own
-    // columns), in a pass of their own right after the update, while the deltas are
-    // live: the deltas of the states / dynamics-row duals go through na / nb (free
-    // between the sweeps); the per-wave partials land in red[32 wv + 16 ..] and are
-    // combined by update_info(INF) after its barrier, which also turns them into the
-    // uniform flags (each test only where its residual test fails, as osqp's
-    // check_termination).
+    // columns), evaluated the way osqp evaluates them: the cheap conditions first
+    // (||E dy||, u'dy+ + l'dy-, ||D dx||, ||D^-1 P dx||), the products A' dy / A dx
+    // only where those hold.  infeas_cheap runs right after the update, while the
+    // deltas are live: it publishes them (na / nb, free between the sweeps) with
+    // update_info's states / duals under one barrier and leaves the per-wave partials
+    // of the cheap quantities in red[32 wv + 16 ..]; update_info(INF) combines them
+    // into uniform flags (each test only where its residual test fails, as osqp's
+    // check_termination); infeas_products, only when a flag holds, adds the products
+    // (two more barriers).  On MPC.py's QPs the dual side never reaches its product
+    // and the primal side does at ~40 % of the checks (oracle counts, C2 batch), so
+    // the product pass is skipped at most checks -- with identical outcomes.
     // outcome bits (one uniform int: the loop carries it): 1 primal, 2 dual infeasible
     // at the check's tolerances, 4 / 8 at the approximate (x10) ones
     int inf_bits = 0;
-    auto infeas_pass = [&](const double (&dy)[3], double dxf, double dxX) __attribute__((always_inline)) {
-      double dyp[3];  // delta_y projected onto the polar of the recession cone of [l, u]
+    int inf_need = 0;  // cheap-condition bits (same layout) awaiting the products
+    double dyp[3];     // delta_y projected onto the polar of the recession cone of [l, u]
+    auto infeas_cheap = [&](const double (&dy)[3], double dxf, double dxX) __attribute__((always_inline)) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const bool uinf = hi_of(j) > kInf * kMinScaling, linf = lo_of(j) < -kInf * kMinScaling;
@@ -1154,38 +1160,25 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         sh.u.it.yv[k][ph] = xX;
         sh.u.it.bo[k][ph] = y[0];
       }
-      sync_all();
-      launder_p();
-      double ndy = 0.0, vu = -INFINITY, vl = -INFINITY, ineq = 0.0;
-      {
-        double adx[3];
-        rowA(dxf, dxX, (lds_cd*)&sh.u.it.na[0][0], adx);
+      double ndy = 0.0, ineq = 0.0;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const double lj = lo_of(j), hj = hi_of(j), v = adx[j] / E[j];
-          ndy = fmax(ndy, fabs(E[j] * dyp[j]));
-          ineq += hj * fmax(dyp[j], 0.0) + lj * fmin(dyp[j], 0.0);
-          if (hj < kInf * kMinScaling) vu = fmax(vu, v);
-          if (lj > -kInf * kMinScaling) vl = fmax(vl, -v);
-        }
+      for (int j = 0; j < 3; ++j) {
+        const double lj = lo_of(j), hj = hi_of(j);
+        ndy = fmax(ndy, fabs(E[j] * dyp[j]));
+        ineq += hj * fmax(dyp[j], 0.0) + lj * fmin(dyp[j], 0.0);
       }
-      double q3[3] = {0.0, 0.0, 0.0};
-      {
-        double dtf, dtX;
-        colAt(dyp, &sh.u.it.nb[0][0], dtf, dtX);
-        if (cl) {
-          const double dif = 1.0 / Df, diX = 1.0 / DX;
-          q3[0] = fmax(fabs(dtf * dif), fabs(dtX * diX));                  // ||D^-1 A' dy||
-          q3[1] = fmax(fabs(Df * dxf), fabs(DX * dxX));                    // ||D dx||
-          q3[2] = fmax(fabs(Pbf() * dxf * dif), fabs(PbX() * dxX * diX));  // ||D^-1 P dx||
-        }
+      double q3[2] = {0.0, 0.0};
+      if (cl) {
+        const double dif = 1.0 / Df, diX = 1.0 / DX;
+        q3[0] = fmax(fabs(Df * dxf), fabs(DX * dxX));                    // ||D dx||
+        q3[1] = fmax(fabs(Pbf() * dxf * dif), fabs(PbX() * dxX * diX));  // ||D^-1 P dx||
       }
-      // maxima over the wave (lanes 0..5 keep quantity s), the sum by xor butterflies
-      double mx[6] = {ndy, q3[0], q3[1], q3[2], vu, vl}, mine = 0.0;
+      // maxima over the wave (lanes 0, 2, 3 keep quantity s), the sum by xor butterflies
+      double mx[3] = {ndy, q3[0], q3[1]}, mine = 0.0;
 #pragma unroll
-      for (int e = 0; e < 6; ++e) {
+      for (int e = 0; e < 3; ++e) {
         const double v = row_max(mx[e]);
-        mine = s == e ? v : mine;
+        mine = s == (e == 0 ? 0 : e + 1) ? v : mine;
       }
       mine = pair_max(row_pair_max(mine));
       ineq += dppd<0xB1>(ineq);
@@ -1200,16 +1193,64 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         ineq = __longlong_as_double(((long long)hi_[0] << 32) | lo_[0]) +
                __longlong_as_double(((long long)hi_[1] << 32) | lo_[1]);
       }
-      if (lane < 6) sh.red[32 * wv + 16 + lane] = mine;
+      if (lane == 0 || lane == 2 || lane == 3) sh.red[32 * wv + 16 + lane] = mine;
       if (lane == 6) sh.red[32 * wv + 16 + 6] = ineq;
-      // (update_info's first barrier publishes these)
+      sync_all();  // (update_info(INF) relies on this barrier for its own publication)
+    };
+    // the products, where a cheap condition holds (inf_need != 0, uniform): A' dy for
+    // the primal test, A dx for the dual one, on the deltas infeas_cheap published
+    auto infeas_products = [&](double dxf, double dxX) __attribute__((always_inline)) {
+      launder_p();
+      double vu = -INFINITY, vl = -INFINITY;
+      {
+        double adx[3];
+        rowA(dxf, dxX, (lds_cd*)&sh.u.it.na[0][0], adx);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const double lj = lo_of(j), hj = hi_of(j), v = adx[j] / E[j];
+          if (hj < kInf * kMinScaling) vu = fmax(vu, v);
+          if (lj > -kInf * kMinScaling) vl = fmax(vl, -v);
+        }
+      }
+      double naty = 0.0;
+      {
+        double dtf, dtX;
+        colAt(dyp, &sh.u.it.nb[0][0], dtf, dtX);
+        if (cl) naty = fmax(fabs(dtf * (1.0 / Df)), fabs(dtX * (1.0 / DX)));  // ||D^-1 A' dy||
+      }
+      double mx[3] = {naty, vu, vl}, mine = 0.0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const double v = row_max(mx[e]);
+        mine = s == (e == 0 ? 1 : e + 3) ? v : mine;
+      }
+      mine = pair_max(row_pair_max(mine));
+      if (lane == 1 || lane == 4 || lane == 5) sh.red[32 * wv + 16 + lane] = mine;
+      sync_all();
+      const int e = s < 6 ? s : 0;  // slots 16..21 are all maxima (0 / 2 / 3 from infeas_cheap)
+      double v = sh.red[16 + e];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) v = fmax(v, sh.red[32 * w + 16 + e]);
+      const double ndy = rbc<0>(v), ndx = rbc<2>(v);  // (the cheap maxima, kept in slots 0 / 2)
+      const double naty_ = rbc<1>(v), vu_ = rbc<4>(v), vl_ = rbc<5>(v);
+      int bits = 0;
+#pragma unroll
+      for (int fi = 0; fi < 2; ++fi) {
+        const double f = fi == 0 ? 1.0 : 10.0, epi = f * p.eps_prim_inf, edi = f * p.eps_dual_inf;
+        const bool pi = ((inf_need >> (2 * fi)) & 1) && naty_ < epi * ndy;
+        const bool di = ((inf_need >> (2 * fi)) & 2) && !(vu_ > edi * ndx) && !(vl_ > edi * ndx);
+        bits |= (pi ? 1 : 0) << (2 * fi);
+        bits |= (di ? 2 : 0) << (2 * fi);
+      }
+      inf_bits = __builtin_amdgcn_readfirstlane(bits);
+      sync_all();
     };
     // The states and dynamics-row duals are published in yv / bo, which the sweeps
     // no longer need (xs still feeds the force recovery of slower waves); lane s
     // of each row then owns residual quantity s, reduced over the wave's rows by
     // permlane swaps and over the waves through red[].  INF: also combine the
-    // partials of infeas_pass.
-    // INF: after infeas_pass, which has published the states / duals with its deltas
+    // cheap partials of infeas_cheap into inf_need.
+    // INF: after infeas_cheap, which has published the states / duals with its deltas
     auto update_info = [&](auto inf_tag) __attribute__((always_inline)) {
       constexpr bool INF = decltype(inf_tag)::value;
       if constexpr (!INF) {
@@ -1285,7 +1326,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       eps_dua = uni(eps_dua); s_pri = uni(s_pri); s_dua = uni(s_dua);
 
       if constexpr (INF) {
-        const int e = s < 7 ? s : 0;
+        // the cheap conditions of infeas_cheap: slots 0 ||E dy||, 2 ||D dx||, 3 ||D^-1 P dx||, 6 u'dy+ + l'dy-
+        const int e = s == 2 || s == 3 || s == 6 ? s : 0;
         double v = sh.red[16 + e];
 #pragma unroll
         for (int w = 1; w < NW; ++w) {
@@ -1295,19 +1337,19 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         // kept in VGPRs (every lane holds the same values) and folded into one uniform
         // int at the end: SGPRs here would push loop-carried scalars into VGPR lanes
         // (v_readlane on the hot path, measured)
-        const double ndy = rbc<0>(v), naty = rbc<1>(v), ndx = rbc<2>(v), npdx = rbc<3>(v);
-        const double vu = rbc<4>(v), vl = rbc<5>(v), ineq = rbc<6>(v);
-        int bits = 0;
+        const double ndy = rbc<0>(v), ndx = rbc<2>(v), npdx = rbc<3>(v), ineq = rbc<6>(v);
+        int need = 0;
 #pragma unroll
         for (int fi = 0; fi < 2; ++fi) {
           const double f = fi == 0 ? 1.0 : 10.0, epi = f * p.eps_prim_inf, edi = f * p.eps_dual_inf;
-          const bool pi = !(pri_res < f * eps_pri) && ndy > kDivTol && ineq < epi * ndy && naty < epi * ndy;
+          const bool pi = !(pri_res < f * eps_pri) && ndy > kDivTol && ineq < epi * ndy;
           const bool di = !(dua_res < f * eps_dua) && ndx > kDivTol && 0.0 < cscale * edi * ndx &&
-                          npdx < cscale * edi * ndx && !(vu > edi * ndx) && !(vl > edi * ndx);
-          bits |= (pi ? 1 : 0) << (2 * fi);
-          bits |= (di ? 2 : 0) << (2 * fi);
+                          npdx < cscale * edi * ndx;
+          need |= (pi ? 1 : 0) << (2 * fi);
+          need |= (di ? 2 : 0) << (2 * fi);
         }
-        inf_bits = __builtin_amdgcn_readfirstlane(bits);
+        inf_need = __builtin_amdgcn_readfirstlane(need);
+        inf_bits = 0;
       }
       sync_all();
     };
@@ -1802,8 +1844,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           last_checked = can_check;
           // the last iteration's information is always formed here, while its deltas are
           // live (osqp's update_info after the loop when the last iteration was unchecked)
-          infeas_pass(dyv, dxf_, dxX_);
+          infeas_cheap(dyv, dxf_, dxX_);
           update_info(std::true_type{});
+          if (inf_need) infeas_products(dxf_, dxX_);
           if (!(isfinite(pri_res) && isfinite(dua_res))) { status = MPCQ_STATUS_NONFINITE; break; }
           if (can_check) {  // osqp check_termination
             if (converged(1.0)) { status = MPCQ_STATUS_SOLVED; break; }

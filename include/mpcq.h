@@ -149,7 +149,10 @@ int mpcq_formulate_batch(mpcq_ctx* ctx, int64_t batch, const double* xref,
  * warm_x [B][n], warm_y [B][m], rho_in [B] are optional (NULL = cold start,
  * rho = params.rho).  x, y, rho_out, iters optional outputs (NULL = skip).
  * info [B][4] (optional): rho updates (refactorisations after the first),
- * polish result (0 not run, 1 accepted, -1 rejected), polish rounds run, 0. */
+ * polish result (0 not run, 1 accepted, -1 rejected), polish rounds run, and
+ * the ADMM's own exit status before polish (with polish = 2 a MAX_ITER /
+ * SOLVED_INACCURATE exit that polish upgrades reports SOLVED in status and the
+ * ADMM's code here). */
 int mpcq_qp_solve_batch(mpcq_ctx* ctx, int64_t batch, const double* Ax,
                         const double* l, const double* u, const double* warm_x,
                         const double* warm_y, const double* rho_in, double* x,
@@ -284,10 +287,13 @@ int mpcq_session_tick(mpcq_session* s, int k, const double* state, const double*
 #define MPCQ_SV_L_FEET 13   /* [B][3][4]   the virtual robot's next feet */
 #define MPCQ_SV_ROT_FLAG 14 /* [B] int32 */
 #define MPCQ_SV_H_ROT 15    /* [B] */
-#define MPCQ_SV_COUNT 16
+#define MPCQ_SV_ORDER 16    /* [B] int32: the next tick's dispatch order (read-only: a permutation of
+                               0..B-1, longest previous solve first, buckets of 16 iterations) */
+#define MPCQ_SV_COUNT 17
 /* Copy array `what` to dst (host, or device with MPCQ_FLAG_DEVICE_PTRS); blocking. */
 int mpcq_session_read(mpcq_session* s, int what, void* dst, uint32_t flags);
-/* Overwrite array `what` from src (host, or device with MPCQ_FLAG_DEVICE_PTRS); blocking. */
+/* Overwrite array `what` from src (host, or device with MPCQ_FLAG_DEVICE_PTRS); blocking.
+ * MPCQ_SV_ORDER is read-only (MPCQ_E_INVALID). */
 int mpcq_session_write(mpcq_session* s, int what, const void* src, uint32_t flags);
 /* Device address of array `what` (valid until mpcq_session_destroy). */
 int mpcq_session_device_ptr(mpcq_session* s, int what, void** out);

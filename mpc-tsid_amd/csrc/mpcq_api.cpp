@@ -559,6 +559,7 @@ size_t sv_bytes(int what, int64_t B, int N) {
     case MPCQ_SV_L_FEET: return b * 12 * 8;
     case MPCQ_SV_ROT_FLAG: return b * 4;
     case MPCQ_SV_H_ROT: return b * 8;
+    case MPCQ_SV_ORDER: return b * 4;
   }
   return 0;
 }
@@ -587,7 +588,7 @@ int mpcq_session_create(mpcq_ctx* c, int64_t B, const mpcq_planner_params* pp, c
   for (int w = 0; w < MPCQ_SV_COUNT; ++w) { s->bytes[w] = sv_bytes(w, B, N); off[w] = take(s->bytes[w]); }
   const size_t o_wx = take((size_t)B * 24 * N * 8), o_ps = take((size_t)B * 4), o_in = take((size_t)B * 16),
                o_st = take((size_t)B * 96), o_lf = take((size_t)B * 96), o_vr = take((size_t)B * 48),
-               o_rd = take((size_t)B * 4), o_or = take((size_t)B * 4);
+               o_rd = take((size_t)B * 4);
   DeviceGuard g(c->device);
   if (hipMalloc(&s->mem, tot) != hipSuccess) {
     delete s;
@@ -607,7 +608,7 @@ int mpcq_session_create(mpcq_ctx* c, int64_t B, const mpcq_planner_params* pp, c
   s->in_lfeet = (double*)(base + o_lf);
   s->in_vref = (double*)(base + o_vr);
   s->in_reduced = (int32_t*)(base + o_rd);
-  s->order = (int32_t*)(base + o_or);
+  s->order = (int32_t*)s->arr[MPCQ_SV_ORDER];
   {
     const char* e = getenv("MPCQ_DISPATCH_ORDER");
     s->use_order = !(e && e[0] == '0');
@@ -818,6 +819,8 @@ int mpcq_session_read(mpcq_session* s, int what, void* dst, uint32_t flags) {
 int mpcq_session_write(mpcq_session* s, int what, const void* src, uint32_t flags) {
   if (!s || !src) return fail(MPCQ_E_INVALID, "NULL argument");
   if (what < 0 || what >= MPCQ_SV_COUNT) return fail(MPCQ_E_INVALID, "unknown session array %d", what);
+  // the engine indexes robots through the order: only order_kernel writes it
+  if (what == MPCQ_SV_ORDER) return fail(MPCQ_E_INVALID, "MPCQ_SV_ORDER is read-only");
   DeviceGuard g(s->ctx->device);
   const hipMemcpyKind kind = (flags & MPCQ_FLAG_DEVICE_PTRS) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   HIP_TRY(hipMemcpyAsync(s->arr[what], src, s->bytes[what], kind, s->ctx->stream));

@@ -730,7 +730,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     for (int j = 0; j < 12; ++j) Fr[j] = 0.0;
     unsigned cls = 0u;
     double cscale = 1.0;
-    int it_done = 0, n_upd = 0, pol_st = 0, pol_rounds = 0;
+    int it_done = 0, n_upd = 0, pol_st = 0, pol_rounds = 0, admm_st = 0;
 #ifdef MPCQ_FACTIME
     uint64_t fac_cycles = 0;
 #endif
@@ -1885,6 +1885,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
                                    : MPCQ_STATUS_MAX_ITER_REACHED;
       }
 
+      admm_st = status;
       // ------------------------------------------------------------ polish
       // OSQP 0.6 polish (polish.c): guess the active set from (z, y), solve the
       // equality-constrained QP  min 1/2 x'Px  s.t. A_act x = b_act,  project
@@ -1906,7 +1907,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           constexpr double kPolishRho = 1e3;
           // the refinement contracts by the error of the explicit stage inverses, which
           // grows with the chain length: 10 steps land within 2e-10 of x* up to N = 32,
-          // N = 48 needs 20 (measured: 10 -> 2-4e-7, 20 -> 1e-10, tools/polish48b.py)
+          // N = 48 needs 20 (measured: 10 -> 2-4e-7, 20 -> 1e-10, tools/attic/polish48b.py)
           constexpr int kPolishMinIter = N > 32 ? 20 : 10;
           const double a_pri = pri_res, a_dua = dua_res;
           const double axf = xf, axX = xX;
@@ -2094,7 +2095,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #else
         a.info[4 * b + 2] = pol_rounds;
 #endif
-        a.info[4 * b + 3] = 0;
+        a.info[4 * b + 3] = admm_st != 0 ? admm_st : status;  // the ADMM's exit status before polish
       }
     }
   }

@@ -13,7 +13,7 @@ from . import synth  # noqa: F401
 from ._lib import (FLAG_ASYNC, FLAG_DEVICE_PTRS, MODE_SETUP, MODE_UPDATE,  # noqa: F401
                    PLAN_FOOTSTEPS, PLAN_REFSTATES, PLAN_ROLL, PLAN_TICK, PlannerParams,
                    default_planner_params, STATUS_BAD_GAIT, SV_COST, SV_F0, SV_FSTEPS, SV_GAIT,
-                   SV_H_ROT, SV_ITERS, SV_L_FEET, SV_Q_W, SV_RHO, SV_ROT_FLAG, SV_STATE, SV_STATUS, SV_X,
+                   SV_H_ROT, SV_ITERS, SV_ORDER, SV_L_FEET, SV_Q_W, SV_RHO, SV_ROT_FLAG, SV_STATE, SV_STATUS, SV_X,
                    SV_X_ROBOT, SV_XREF, SV_Y, STATUS_FACTOR_FAILED, STATUS_MAX_ITER_REACHED,
                    STATUS_NONFINITE, STATUS_SOLVED, STATUS_SOLVED_INACCURATE, STATUS_PRIMAL_INFEASIBLE,
                    STATUS_DUAL_INFEASIBLE, STATUS_PRIMAL_INFEASIBLE_INACCURATE,

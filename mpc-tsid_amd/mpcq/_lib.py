@@ -58,6 +58,7 @@ PLAN_TICK = PLAN_ROLL | PLAN_FOOTSTEPS | PLAN_REFSTATES
 # closed-loop session arrays (MPCQ_SV_*)
 SV_F0, SV_X, SV_X_ROBOT, SV_Q_W, SV_COST, SV_XREF, SV_FSTEPS, SV_GAIT = range(8)
 SV_STATUS, SV_ITERS, SV_RHO, SV_Y, SV_STATE, SV_L_FEET, SV_ROT_FLAG, SV_H_ROT = range(8, 16)
+SV_ORDER = 16  # read-only: the next tick's dispatch order
 
 EXPORTS = ("mpcq_abi_version", "mpcq_default_params", "mpcq_dims", "mpcq_pattern",
            "mpcq_supported_horizons", "mpcq_last_error", "mpcq_create", "mpcq_destroy",

@@ -131,7 +131,8 @@ class Engine:
         info = np.empty((B, 4), np.int32)
         self._call("mpcq_qp_solve_batch", self._h, B, _p(Ax), _p(l), _p(u), _p(wx), _p(wy), _p(rho_in),
                                             _p(x), _p(y), _p(st), _p(it), _p(ro), _p(info), 0)
-        return dict(x=x, y=y, status=st, iters=it, rho=ro, rho_updates=info[:, 0], polish=info[:, 1])
+        return dict(x=x, y=y, status=st, iters=it, rho=ro, rho_updates=info[:, 0], polish=info[:, 1],
+                    polish_rounds=info[:, 2], admm_status=info[:, 3])
 
     def solve(self, xref, fsteps, mode: int = L.MODE_UPDATE, warm_x=None, warm_y=None, rho=None,
               want_x: bool = True, want_y: bool = False):
@@ -150,7 +151,8 @@ class Engine:
         info = np.empty((B, 4), np.int32)
         self._call("mpcq_solve_batch", self._h, B, _p(xref), _p(fsteps), mode, _p(wx), _p(wy), _p(rin), _p(f0),
                                          _p(x), _p(y), _p(rout), _p(st), _p(it), _p(info), 0)
-        return dict(f0=f0, x=x, y=y, rho=rout, status=st, iters=it, rho_updates=info[:, 0], polish=info[:, 1])
+        return dict(f0=f0, x=x, y=y, rho=rout, status=st, iters=it, rho_updates=info[:, 0], polish=info[:, 1],
+                    polish_rounds=info[:, 2], admm_status=info[:, 3])
 
     # ------------------------------------------------------------------ footstep planner
     def plan(self, ops: int, k: int, state, l_feet, v_ref, gait, rot_flag, h_rot, xref, fsteps,

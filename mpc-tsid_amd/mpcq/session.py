@@ -30,6 +30,7 @@ def _shapes(B, N):
         L.SV_STATUS: ((B,), np.int32), L.SV_ITERS: ((B,), np.int32), L.SV_RHO: ((B,), np.float64),
         L.SV_Y: ((B, 44 * N), np.float64), L.SV_STATE: ((B, 12), np.float64),
         L.SV_L_FEET: ((B, 3, 4), np.float64), L.SV_ROT_FLAG: ((B,), np.int32), L.SV_H_ROT: ((B,), np.float64),
+        L.SV_ORDER: ((B,), np.int32),
     }
 
 

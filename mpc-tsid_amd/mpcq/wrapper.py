@@ -104,7 +104,9 @@ class MPC:
         self.xref = xref
         self.x0 = xref[:, 0:1]
         mode = L.MODE_SETUP if k == 0 else L.MODE_UPDATE
-        xr = np.ascontiguousarray(xref)[None]
+        # copies: the caller's planner rewrites xref / fsteps in place every tick
+        # (FootstepPlanner.py:96-156), and ML / NK / NK_inf are formed from these later
+        xr = np.array(xref, dtype=np.float64, copy=True)[None]
         fs = np.array(fsteps, dtype=np.float64, copy=True)[None]
         if k == 0:
             r = self.engine.solve(xr, fs, mode, want_x=True, want_y=True)

@@ -756,7 +756,8 @@ static int polish(Work* W, const mpcq_params* p, Info* admm_info, double* x, dou
 }
 
 /* info_out: [0] iterations, [1] rho updates (refactorisations beyond the
- * first), [2] polish status (0 not run, 1 ok, -1 rejected) */
+ * first), [2] polish status (0 not run, 1 ok, -1 rejected), [3] the ADMM's own
+ * status before polish (polish = 2 may upgrade it to SOLVED) */
 int oracle_qp_solve(const mpcq_params* p, int N, const double* Ax, const double* l,
                     const double* u, const double* warm_x, const double* warm_y,
                     const double* rho_in, double* x_out, double* y_out, int32_t* status,
@@ -765,7 +766,7 @@ int oracle_qp_solve(const mpcq_params* p, int N, const double* Ax, const double*
   if (work_init(&Wk, N) != 0) { work_free(&Wk); return -1; }
   Work* W = &Wk;
   int n = W->n, m = W->m;
-  int st = 0, it_done = 0, n_upd = 0, pol = 0;
+  int st = 0, it_done = 0, n_upd = 0, pol = 0, admm_st = 0;
   double rho = p->rho;
   /* data (MPC.py:236-288 cost; python osqp clamps bounds to +-OSQP_INFTY) */
   for (int c = 0; c < n; ++c) W->Pd[c] = (c < 12 * N) ? p->state_weights[c % 12] : p->force_weight;
@@ -846,6 +847,7 @@ int oracle_qp_solve(const mpcq_params* p, int N, const double* Ax, const double*
     if (st == 0) st = check_termination(W, &I, p, 1);
     if (st == 0) st = MPCQ_STATUS_MAX_ITER_REACHED;
   }
+  admm_st = st;
   /* polish == 1: OSQP (only after SOLVED); polish == 2: also after an inaccurate
    * or max-iter exit, upgrading the status when the polished point meets eps. */
   if (p->polish && (st == MPCQ_STATUS_SOLVED ||
@@ -859,6 +861,7 @@ int oracle_qp_solve(const mpcq_params* p, int N, const double* Ax, const double*
     }
   }
 out:
+  if (admm_st == 0) admm_st = st; /* the data checks' exits */
   if (x_out) for (int c = 0; c < n; ++c) x_out[c] = W->D[c] * W->x[c];
   if (y_out) for (int r = 0; r < m; ++r) y_out[r] = p->dual_warm ? W->y[r] : W->E[r] * W->y[r] / W->c;
   if (st == MPCQ_STATUS_NONFINITE || st == MPCQ_STATUS_FACTOR_FAILED || st == MPCQ_STATUS_BAD_BOUNDS) {
@@ -873,15 +876,16 @@ out:
   if (status) *status = st;
   if (iters) *iters = it_done;
   if (rho_out) *rho_out = rho;
-  if (info_out) { info_out[0] = it_done; info_out[1] = n_upd; info_out[2] = pol; }
+  if (info_out) { info_out[0] = it_done; info_out[1] = n_upd; info_out[2] = pol; info_out[3] = admm_st; }
   work_free(W);
   return 0;
 }
 
-/* fused formulation + solve for a batch (OpenMP over instances). */
+/* fused formulation + solve for a batch (OpenMP over instances); info [B][4]
+ * (optional) as oracle_qp_solve's info_out. */
 int oracle_solve_batch(const mpcq_params* p, int N, int64_t B, const double* xref,
                        const double* fsteps, int mode, double* f0, double* x_out,
-                       int32_t* status, int32_t* iters, int nthreads) {
+                       int32_t* status, int32_t* iters, int32_t* info, int nthreads) {
   int32_t n, m, nnz;
   oracle_dims(N, &n, &m, &nnz);
 #ifdef _OPENMP
@@ -897,14 +901,16 @@ int oracle_solve_batch(const mpcq_params* p, int N, int64_t B, const double* xre
     double* x = malloc(8 * (size_t)n);
 #pragma omp for schedule(dynamic, 1)
     for (int64_t b = 0; b < B; ++b) {
-      int32_t st = 0, it = 0;
+      int32_t st = 0, it = 0, inf4[4] = {0, 0, 0, 0};
       int fs = oracle_formulate(p, N, xref + b * 12 * (N + 1), fsteps + b * 260, mode, Ax, l, u);
       if (fs != 0) {
         st = fs;
+        inf4[3] = fs;
         for (int c = 0; c < n; ++c) x[c] = NAN;
       } else {
-        oracle_qp_solve(p, N, Ax, l, u, NULL, NULL, NULL, x, NULL, &st, &it, NULL, NULL);
+        oracle_qp_solve(p, N, Ax, l, u, NULL, NULL, NULL, x, NULL, &st, &it, NULL, inf4);
       }
+      if (info) memcpy(info + 4 * b, inf4, sizeof inf4);
       if (f0) memcpy(f0 + 12 * b, x + 12 * N, 12 * 8);
       if (x_out) memcpy(x_out + b * n, x, 8 * (size_t)n);
       if (status) status[b] = st;

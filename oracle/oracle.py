@@ -95,7 +95,7 @@ def _bind(path: str):
     L.oracle_qp_solve.argtypes = [C.POINTER(Params), C.c_int, dp, dp, dp, dp, dp, dp,
                                   dp, dp, ip, ip, dp, ip]
     L.oracle_solve_batch.argtypes = [C.POINTER(Params), C.c_int, C.c_int64, dp, dp, C.c_int,
-                                     dp, dp, ip, ip, C.c_int]
+                                     dp, dp, ip, ip, ip, C.c_int]
     L.oracle_num_threads.restype = C.c_int
     L.oracle_default_planner_params.argtypes = [C.POINTER(PlannerParams)]
     L.oracle_retrieve.argtypes = [C.POINTER(Params), C.c_int, dp, dp, dp, dp, dp, C.c_int,
@@ -176,7 +176,8 @@ def formulate(xref, fsteps, mode: int = 0, params: Params | None = None):
 
 
 def qp_solve(N, Ax, l, u, params: Params | None = None, warm_x=None, warm_y=None, rho=None):
-    """One QP: returns dict(x, y, status, iters, rho, rho_updates, polish)."""
+    """One QP: returns dict(x, y, status, iters, rho, rho_updates, polish, admm_status);
+    admm_status is the ADMM's exit status before polish (polish = 2 may upgrade it)."""
     n, m, nnz = dims(N)
     Ax = np.ascontiguousarray(Ax, np.float64)
     l = np.ascontiguousarray(l, np.float64)
@@ -186,7 +187,7 @@ def qp_solve(N, Ax, l, u, params: Params | None = None, warm_x=None, warm_y=None
     st = np.zeros(1, np.int32)
     it = np.zeros(1, np.int32)
     rho_out = np.zeros(1)
-    info = np.zeros(3, np.int32)
+    info = np.zeros(4, np.int32)
     rho_in = None if rho is None else np.array([rho], np.float64)
     wx = None if warm_x is None else np.ascontiguousarray(warm_x, np.float64)
     wy = None if warm_y is None else np.ascontiguousarray(warm_y, np.float64)
@@ -194,13 +195,14 @@ def qp_solve(N, Ax, l, u, params: Params | None = None, warm_x=None, warm_y=None
     lib().oracle_qp_solve(C.byref(p), N, _dp(Ax), _dp(l), _dp(u), _dp(wx), _dp(wy), _dp(rho_in),
                           _dp(x), _dp(y), _ip(st), _ip(it), _dp(rho_out), _ip(info))
     return dict(x=x, y=y, status=int(st[0]), iters=int(it[0]), rho=float(rho_out[0]),
-                rho_updates=int(info[1]), polish=int(info[2]))
+                rho_updates=int(info[1]), polish=int(info[2]), admm_status=int(info[3]))
 
 
 def solve_batch(xref, fsteps, mode: int = 0, params: Params | None = None, nthreads: int = 0,
                 want_x: bool = False, native: bool = False):
     """Batched formulation + solve on host threads (OpenMP); native=True runs the
-    -O3 -march=native baseline build (timing only)."""
+    -O3 -march=native baseline build (timing only).  Also returns rho_updates, polish
+    (0 not run, 1 accepted, -1 rejected) and admm_status (before polish) per instance."""
     xref = np.ascontiguousarray(xref, np.float64)
     fsteps = np.ascontiguousarray(fsteps, np.float64)
     B = xref.shape[0]
@@ -210,10 +212,11 @@ def solve_batch(xref, fsteps, mode: int = 0, params: Params | None = None, nthre
     x = np.zeros((B, n)) if want_x else None
     st = np.zeros(B, np.int32)
     it = np.zeros(B, np.int32)
+    info = np.zeros((B, 4), np.int32)
     p = params or default_params()
     (native_lib() if native else lib()).oracle_solve_batch(C.byref(p), N, B, _dp(xref), _dp(fsteps), mode,
-                                                          _dp(f0), _dp(x), _ip(st), _ip(it), nthreads)
-    return dict(f0=f0, x=x, status=st, iters=it)
+                                                          _dp(f0), _dp(x), _ip(st), _ip(it), _ip(info), nthreads)
+    return dict(f0=f0, x=x, status=st, iters=it, rho_updates=info[:, 1], polish=info[:, 2], admm_status=info[:, 3])
 
 
 def default_planner_params(**overrides) -> PlannerParams:

@@ -15,6 +15,9 @@ class OracleEngine:
         self.calls = []
 
     def formulate(self, xref, fsteps, mode=0):
+        xref, fsteps = np.asarray(xref), np.asarray(fsteps)
+        if xref.ndim == 3:  # a batch of one, as Engine.formulate takes it
+            xref, fsteps = xref[0], fsteps[0]
         try:
             Ax, l, u = self.O.formulate(xref, fsteps, mode, self.oparams)
             st = 0

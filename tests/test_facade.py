@@ -49,6 +49,22 @@ def test_tick_sequence_and_attributes(wrapper, golden16, oracle):
     assert np.array_equal(r["x"], m.x)
 
 
+def test_formulation_attributes_keep_the_solved_qp(wrapper, golden16, oracle):
+    """ML / NK / NK_inf describe the QP run() solved, even after the caller's planner
+    rewrites xref / fsteps in place for the next tick (FootstepPlanner.py:96-156)."""
+    w, N = wrapper, 16
+    pl = Planner(golden16["xref"][0], golden16["fsteps"][0])
+    w.solve(0, pl)
+    w.solve(20, pl)
+    Ax, l, u = oracle.formulate(golden16["xref"][0], np.nan_to_num(golden16["fsteps"][0]), 0)
+    pl.xref += 0.05           # the planner's in-place update of the next tick
+    pl.fsteps[:, 1:] += 0.01
+    m = w.mpc
+    assert np.array_equal(m.ML.data, Ax)
+    assert np.array_equal(m.NK.ravel(), u)
+    assert np.array_equal(m.NK_inf, l)
+
+
 def test_run_mpc_alias_and_virtual(oracle, golden16):
     from mpcq.wrapper import MPC_Virtual, MPC_Wrapper
     w = MPC_Wrapper(0.02, 16, 20, 0.32, engine=OracleEngine(oracle))

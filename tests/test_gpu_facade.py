@@ -34,7 +34,8 @@ def test_solve_batch(golden16, oracle):
     f0, info = w.solve_batch(golden16["xref"][:8], golden16["fsteps"][:8])
     ref = oracle.solve_batch(golden16["xref"][:8], golden16["fsteps"][:8], 0, nthreads=4)
     assert np.array_equal(info["status"], ref["status"])
-    assert np.abs(f0 - ref["f0"]).max() < 1e-6
+    assert np.array_equal(info["iters"], ref["iters"])
+    assert np.abs(f0 - ref["f0"]).max() < 1e-9  # same algorithm, fp64 rounding only (observed ~1e-12)
 
 
 def test_footstep_planner_facade_vs_reference_fixtures():

@@ -196,6 +196,7 @@ def test_session_dispatch_order_changes_no_result(mpcq, monkeypatch, N):
                       rng.uniform(-.5, .5, B)], axis=1)
     names = ("SV_F0", "SV_X", "SV_Y", "SV_STATUS", "SV_ITERS", "SV_RHO", "SV_STATE", "SV_Q_W", "SV_COST")
     runs = {}
+    orders = []
     for flag in ("0", "1"):
         monkeypatch.setenv("MPCQ_DISPATCH_ORDER", flag)
         out = []
@@ -203,9 +204,21 @@ def test_session_dispatch_order_changes_no_result(mpcq, monkeypatch, N):
             for _ in range(T):
                 sess.tick(v_ref)
                 out.append({n: sess.read(getattr(mpcq, n)).copy() for n in names})
+                if flag == "1":
+                    orders.append(sess.read(mpcq.SV_ORDER).copy())
         runs[flag] = out
-    iters = np.array([t["SV_ITERS"] for t in runs["1"]])
-    assert iters[1:].std() > 0  # the order is not the identity
+    # the order each tick leaves for the next: a permutation of the robots, longest
+    # solve of this tick first (buckets of 16 iterations), and not the identity
+    moved = 0
+    for k in range(T):
+        o, it = orders[k], runs["1"][k]["SV_ITERS"]
+        assert np.array_equal(np.sort(o), np.arange(B)), k
+        bucket = np.minimum(np.maximum(it, 0) >> 4, 255)[o]
+        assert (np.diff(bucket) <= 0).all(), k
+        moved += int((o != np.arange(B)).sum())
+        if k > 0:
+            moved += int((o != orders[k - 1]).sum())
+    assert moved > 0
     for k in range(T):
         for n in names:
             assert np.array_equal(runs["0"][k][n], runs["1"][k][n], equal_nan=True), (k, n)

@@ -53,9 +53,19 @@ def test_two_ranks_engine_shards_match_single_process(tmp_path, oracle):
     import torch.multiprocessing as mp
     import mpcq
     out = str(tmp_path / "r0.npz")
+    import time
     ctx = mp.spawn(_worker, args=(2, _free_port(), TOTAL, out), nprocs=2, join=False)
-    while not ctx.join(timeout=60):
-        pass
+    deadline = time.monotonic() + 100  # a blocked rank (rendezvous, gather) fails the test, not the suite
+    done = False
+    while not done and time.monotonic() < deadline:
+        done = ctx.join(timeout=5)
+    if not done:
+        for proc in ctx.processes:
+            if proc.is_alive():
+                proc.terminate()
+        for proc in ctx.processes:
+            proc.join(timeout=10)
+        pytest.fail(f"ranks did not finish in time; exit codes {[proc.exitcode for proc in ctx.processes]}")
     got = np.load(out)
     g = mpcq.synth.make_batch(TOTAL, 16, gaits=("trot", "bound", "pace"), seed=11)
     with mpcq.Engine(16) as e:

@@ -151,11 +151,15 @@ def test_headline_c3_full_batch(mpcq, oracle):
     assert (r["status"] == mpcq.STATUS_SOLVED).all()
     upgraded = (r["admm_status"] != mpcq.STATUS_SOLVED) & (r["status"] == mpcq.STATUS_SOLVED)
     at_max = r["iters"] == 4000
-    assert upgraded.sum() > 0 and (r["admm_status"][at_max] == mpcq.STATUS_MAX_ITER_REACHED).all()
+    # the ADMM's exits at max_iter: SOLVED_INACCURATE (round 3: 51 of 53, the other two meet eps at
+    # the last check), all of them upgraded by polish = 2
+    assert upgraded.sum() > 0 and np.isin(r["admm_status"][at_max], (1, 2, -2)).all()
+    assert upgraded[at_max].sum() == (r["admm_status"][at_max] != 1).sum()
     fstar = _certified(b["xref"], b["fsteps"], r["x"], r["y"])
     dfo = np.abs(r["f0"] - fstar).max(axis=1)
     d_ora = np.abs(r["f0"] - o["f0"]).max()
-    print(f"C3 full batch: {int(upgraded.sum())} instances upgraded by polish ({int(at_max.sum())} at max_iter); "
+    print(f"C3 full batch: {int(upgraded.sum())} instances upgraded by polish ({int(at_max.sum())} at max_iter, ADMM "
+          f"statuses {dict(zip(*np.unique(r['admm_status'], return_counts=True)))}); "
           f"max|f0 - f0*| {dfo.max():.2e} (upgraded ones {dfo[upgraded].max():.2e}), "
           f"max|f0 - f0_oracle| {d_ora:.2e}")
     assert dfo.max() < 1e-8

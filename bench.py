@@ -469,7 +469,7 @@ def main():
         return model.flops(N, r["iters"], r["info"][:, 0], pp.check_termination,
                            pp.adaptive_rho_interval if pp.adaptive_rho else 0, pp.scaling,
                            polish_rounds=r["info"][:, 2] if pp.polish else None,
-                           polish_solves=1 + max(pp.polish_refine_iter, 20 if N > 32 else 10),
+                           polish_solves=1 + max(pp.polish_refine_iter, model.polish_min_refinements(N)),
                            structured=structured).sum()
 
     fl, fl_dense = work(head), work(head, structured=False)

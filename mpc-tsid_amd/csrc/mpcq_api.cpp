@@ -258,7 +258,7 @@ int mpcq_create(int device, int n_steps, const mpcq_params* params, mpcq_ctx** o
   if (!out) return fail(MPCQ_E_INVALID, "out is NULL");
   *out = nullptr;
   if (!mpcq::horizon_supported(n_steps))
-    return fail(MPCQ_E_UNSUPPORTED, "horizon N=%d not compiled in (supported: N = 4j, 4 <= N <= 32, and 48)", n_steps);
+    return fail(MPCQ_E_UNSUPPORTED, "horizon N=%d not compiled in (supported: 4 <= N <= 64)", n_steps);
   mpcq_params p;
   if (params) p = *params;
   else mpcq_default_params(&p);

@@ -2,13 +2,13 @@
 // compiled once per horizon (Makefile: -DMPCQ_ENGINE_N=N); each unit exports
 // engine_launch_n<N>, and this file maps a context's N onto it.
 //
-// Horizons compiled in: every N = 4j up to 32, and 48.  One wave64 holds four
-// 16-lane stage rows, so N is a multiple of 4; the reference's n_steps =
-// n_periods * T_gait / dt (FootstepPlanner.py:55) gives N = 8, 16, 24, 32, 48 for
-// the usual dt / n_periods.  N <= 16 fits two instances per CU, 20 <= N <= 32 one
-// (LDS, checked by static_asserts in mpcq_engine.hip); N = 48 keeps S^{-1}, F W
-// and R^{-1} Q in a per-instance global workspace (work_doubles, one instance per
-// CU).
+// Horizons compiled in: every N from 4 to 64 (MPC.py takes any n_steps,
+// MPC.py:22-26; FootstepPlanner.py:55 gives n_periods * T_gait / dt).  A wave64
+// holds four 16-lane stage rows; N that is not a multiple of 4 runs the rows past
+// N as copies of stage N-1 (kRows in mpcq_engine.hip).  Up to 16 stages two
+// instances share a CU, up to 32 one (LDS, checked by static_asserts in
+// mpcq_engine.hip); beyond 32, S^{-1}, F W and R^{-1} Q live in a per-instance
+// global workspace (work_doubles), beyond 56 the scaled constraint values too.
 #include "mpcq_internal.h"
 
 namespace mpcq {

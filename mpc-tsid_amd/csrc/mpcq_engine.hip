@@ -94,6 +94,14 @@ __device__ __forceinline__ int SIG(int k) { return k <= N / 2 ? k : N + N / 2 - 
 template <int N>
 __device__ __forceinline__ int SIGX(int q) { return q <= N / 2 ? q : N + N / 2 + 1 - q; }
 
+// Stage rows of the layout: a wave64 holds four 16-lane rows, so the workgroup
+// has N rounded up to a multiple of 4 rows.  The rows past N ("phantom" rows)
+// run as copies of stage N-1: they read what row N-1 reads and store the same
+// values to the same places (identical stores), are left out of the in-place
+// updates and the sums, and their maxima duplicate row N-1's.
+template <int N>
+constexpr int kRows = (N + 3) & ~3;
+
 // ---------------------------------------------------------------------------
 // cross-lane helpers
 
@@ -424,16 +432,21 @@ __host__ __device__ constexpr int SLOT(int q) { return GS * q + (q > N / 2 ? kSl
 // doubles per instance, L2-resident), the rest stays in LDS (N = 48: 140 KB).
 template <int N>
 constexpr bool kBig = N > 32;
+// Beyond 56 stages the scaled constraint values (126 N - 18 doubles) leave LDS as well
+// (N = 64: 185 KB with them, 121 KB without); the engine reads them through the
+// same accessors, the stage-parallel phases from L2.
+template <int N>
+constexpr bool kAbG = N > 56;
 template <int N>
 struct Work {  // offsets (doubles) inside one instance's workspace
-  // two slots ahead of S^{-1}: the sweep's lagging half reads (and discards) the rows
-  // of slots -2 / -1 in its first steps, which in LDS fall on GH
-  static constexpr int SM = 2 * GS, FW = SM + N * GS + 2, QL = FW + 72 * N, ZERO = QL + 36 * N, SIZE = ZERO + 72;
+  // SM starts two slots in (a pad kept from round 2; the sweep no longer reads it)
+  static constexpr int SM = 2 * GS, FW = SM + N * GS + 2, QL = FW + 72 * N, ZERO = QL + 36 * N, AB = ZERO + 72,
+                       SIZE = AB + (kAbG<N> ? ((126 * N - 18 + 1) & ~1) : 0);
 };
 
 template <int N>
 struct Smem {
-  double Ab[126 * N - 18];  // scaled constraint values, CSC order
+  double Ab[kAbG<N> ? 2 : 126 * N - 18];  // scaled constraint values, CSC order (N > 56: Work<N>::AB)
   // GH[0] = M^{-1}, GH[SIG(k)] = G_k (1 <= k <= m), GH[SIG(k+1)] = H_k (m <= k < N-1),
   // row-major (the sweeps' step order, see SIG).
   // During the factorisation slot k holds Q_k [0,36), F_k W_k [36,108) and the
@@ -461,9 +474,10 @@ struct Smem {
       double St[144], Sb[144];  // sweep hand-offs of the factorisation
     } fa;
   } u;
-  // per-row partial reductions; during the sweeps the sink of lanes whose store is void
-  double red[(12 * N > 12 * (N / 2 + 1) + 64) ? 12 * N : 12 * (N / 2 + 1) + 64];
-  double dump[16 * N];      // per-lane sink: predicated stores write here instead of branching
+  // per-wave partial reductions (32 per wave); during the sweeps the sink of lanes
+  // whose store is void (lane (t & 31) + 12 j, j <= N/2 + 1)
+  double red[(8 * kRows<N> + 32 > 12 * (N / 2 + 2) + 32) ? 8 * kRows<N> + 32 : 12 * (N / 2 + 2) + 32];
+  double dump[64];          // sink of predicated stores (never read): lane & 63
   alignas(16) double zero[72];  // zeros: masked coefficient reads point here instead of selecting
   int flag[4];
 };
@@ -481,23 +495,33 @@ struct Prologue {
 // !FUSED: solve the given (Ax, l, u).  SOLVE=false: formulation only.
 
 template <int N, bool FUSED, bool SOLVE, bool POLISH>
-__global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, LaunchArgs a) {
-  constexpr int NW = N / 4, T = 16 * N, n = 24 * N, m = 44 * N, nnz = 126 * N - 18, MID = N / 2;
+__global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p, LaunchArgs a) {
+  constexpr int NR = kRows<N>, NW = NR / 4, T = 16 * NR, n = 24 * N, m = 44 * N, nnz = 126 * N - 18, MID = N / 2;
+  // the two chains of the state sweeps: top stages 0..MID-1, bottom N-1..MID+1
+  // (BOT stages: MID - 1 for even N, MID for odd N), meeting at stage MID
+  constexpr int BOT = N - 1 - MID;
   __shared__ Smem<N> sh;
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
   // lane coordinates; the loops launder them (see launder()) so that the
   // compiler recomputes the many LDS offsets derived from them instead of
   // hoisting each one into a register of its own
-  int k = t >> 4, s = t & 15, f = s >> 2, c = s & 3;
+  const bool phantom = (t >> 4) >= N;  // a row past the horizon: a copy of stage N-1 (kRows)
+  int k = phantom ? N - 1 : t >> 4, s = t & 15, f = s >> 2, c = s & 3;
   const bool cl = c < 3;          // column lane (c == 3: friction rows 3, 4 only)
   int cc = cl ? c : 2;            // column component; c == 3 shadows c == 2
   int ph = 3 * f + cc;            // own force / state index in the stage
   if ((int64_t)blockIdx.x >= a.batch) return;
   const int64_t b = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;  // the instance
   STAMP_DECL
-  lds_cd* Ab = (lds_cd*)sh.Ab;
+  constexpr bool BIG = kBig<N>, ABG = kAbG<N>;
+  // the scaled constraint values: LDS, or (N > 56) this instance's workspace (the
+  // formulation-only launch builds them straight into its Ax output)
+  using acd = std::conditional_t<ABG, const double, lds_cd>;
+  double* AbW;
+  if constexpr (ABG) AbW = SOLVE ? a.work + b * Work<N>::SIZE + Work<N>::AB : a.Ax_out + b * nnz;
+  else AbW = sh.Ab;
+  acd* Ab = (acd*)AbW;
   lds_cd* GHr = (lds_cd*)&sh.GH[0][0];
-  constexpr bool BIG = kBig<N>;
   // S^{-1}, F W, R^{-1} Q: LDS, or (N > 32) this instance's global workspace
   using wcd = std::conditional_t<BIG, const double, lds_cd>;
   using wdd = std::conditional_t<BIG, double, lds_d>;
@@ -593,12 +617,14 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
   double lo_g[FUSED ? 1 : 3], hi_g[FUSED ? 1 : 3];
   if (t == 0) { sh.flag[0] = 0; sh.flag[1] = 0; sh.flag[2] = 0; sh.flag[3] = 0; }
   for (int e = t; e < 72; e += T) sh.zero[e] = 0.0;  // N = 4: one wave of 64 lanes
-  // The sweep arrays start at zero: a few lanes and steps read slots that are not
-  // (yet) written this launch — the bottom chain's idle last step, the lagging half's
-  // first rows — and discard the products or scale them by zero; LDS left over from
-  // an earlier workgroup can hold NaN / Inf, which a zero factor does not cancel.
-  // (X_0 slot xs[0] included: masked reads multiply it by zero.)
+  // The sweep arrays start at zero.  No read depends on it (round 3): the steps a
+  // sweep chain does not take re-read slots the chain wrote, and stage 0 reads its
+  // absent X_0 terms from sh.zero; the zeroing stays as a guard against LDS left
+  // over from an earlier workgroup (NaN / Inf).  -DMPCQ_NO_LDS_ZERO builds without
+  // it (tools/build_variant.sh nozero ...: the GPU suite must pass on that build).
+#ifndef MPCQ_NO_LDS_ZERO
   for (int e = t; e < (int)(sizeof(sh.u.it) / sizeof(double)); e += T) (&sh.u.it.bo[0][0])[e] = 0.0;
+#endif
 
   // ---------------------------------------------------------------- prologue
   if (FUSED || !SOLVE) {
@@ -635,10 +661,10 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     if (sh.flag[0] == 0) {
       for (int e = t; e < 12 * N; e += T) {  // state columns: -I / A (MPC.py:107-115)
         const int kk = e / 12, i = e % 12, xo = XO<N>(kk, i);
-        sh.Ab[xo] = -1.0;
+        AbW[xo] = -1.0;
         if (kk < N - 1) {
-          if (i >= 6) { sh.Ab[xo + 1] = p.dt; sh.Ab[xo + 2] = 1.0; }
-          else sh.Ab[xo + 1] = 1.0;
+          if (i >= 6) { AbW[xo + 1] = p.dt; AbW[xo + 2] = 1.0; }
+          else AbW[xo + 1] = 1.0;
         }
       }
       for (int e = t; e < 4 * N; e += T) {  // foot q of stage kk
@@ -658,7 +684,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           lv[r] = ft - xr[r * (N + 1) + kk];
         }
         form_foot(p, xr[5 * (N + 1) + kk], lv[0], lv[1], lv[2], 1.0 - (double)con_[4 * j + q],
-                  sh.Ab + FO<N>(kk, q, 0));
+                  AbW + FO<N>(kk, q, 0));
       }
       bnd = dyn_bound<N>(p, xr, k, ph);
     }
@@ -667,7 +693,8 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       if (t == 0 && a.status) a.status[b] = sh.flag[0];
       if (sh.flag[0] != 0) return;
       double* go = a.Ax_out + b * nnz;
-      for (int e = t; e < nnz; e += T) go[e] = sh.Ab[e];
+      if constexpr (!ABG)
+        for (int e = t; e < nnz; e += T) go[e] = sh.Ab[e];
 #pragma unroll
       for (int slot = 0; slot < 3; ++slot) {
         const int r = nat_row(slot);
@@ -688,7 +715,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     }
   } else {
     const double* ga = a.Ax + b * nnz;
-    for (int e = t; e < nnz; e += T) sh.Ab[e] = ga[e];
+    for (int e = t; e < nnz; e += T) AbW[e] = ga[e];
     if constexpr (!FUSED) {
 #pragma unroll
       for (int slot = 0; slot < 3; ++slot) {
@@ -704,7 +731,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     {  // non-finite data -> NONFINITE (the problem is always feasible otherwise)
       int bad = 0;
       for (int e = t; e < nnz; e += T)
-        if (!isfinite(sh.Ab[e])) bad = 1;
+        if (!isfinite(AbW[e])) bad = 1;
       int lgu = 0;  // l > u on an own row (osqp rejects the data)
       if constexpr (FUSED) {
         if (cl && isnan(bnd)) bad = 1;
@@ -1049,18 +1076,23 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
     // the sweep's states in its slots (SIGX): own X_{k+1}, the previous stage's X_k
     const int rXS = 12 * SIGX<N>(k + 1) + ph, rXSp = 12 * SIGX<N>(k) + ph,
               rXSp6 = 12 * SIGX<N>(k) + (ph < 6 ? ph + 6 : ph);
+    const int zXS = (int)(sh.zero - &sh.u.it.xs[0][0]);  // X_0 is not stored: stage 0 reads zeros
+    const int rXSpm = hp ? rXSp : zXS, rXSp6m = hp ? rXSp6 : zXS;
     const double m2 = cc == 2 ? 1.0 : 0.0;
     // masked variants for the loop: a lane whose term is structurally absent reads a
     // zero (stage 0 has no previous stage; H6 only on the position rows; the force Schur
     // terms beta, (R^-1 Q) g only on the velocity rows), so no selects are needed
-    const int oHdm = hp ? oHd : (int)(sh.zero - sh.Ab);
-    const int oH6m = hp && !isv ? oH6 : (int)(sh.zero - sh.Ab);
+    int zAb;  // offset of a zero block from Ab (masked reads)
+    if constexpr (ABG) zAb = Work<N>::ZERO - Work<N>::AB;
+    else zAb = (int)(sh.zero - sh.Ab);
+    const int oHdm = hp ? oHd : zAb;
+    const int oH6m = hp && !isv ? oH6 : zAb;
     const int oFWcm = isv ? oFWc : zFW;
     const int oQLm = isv ? oQL : zQL;
     lds_cd* XSr = (lds_cd*)&sh.u.it.xs[0][0];
     double* const Wbo = &sh.u.it.bo[SIG<N>(k)][ph];
     double* const Wna = &sh.u.it.na[SIG<N>(hp ? k - 1 : N - 1)][ph];
-    double* const Wdump = &sh.dump[t];
+    double* const Wdump = &sh.dump[t & 63];
     const int oB0 = FO<N>(k, 0, 0) + (ph >= 9 ? ph - 8 : 0);  // B row ph on force (fp, cp): + 24 fp + 7 cp
     auto launder_p = [&]() __attribute__((always_inline)) {
       lds_uniform(Ab); lds_uniform(GHr); lds_uniform(SmR); lds_uniform(FWr); lds_uniform(QLr); lds_uniform(XSr);
@@ -1107,8 +1139,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
       }
       const double bfx = bdot_ln12(bco, vf, 0.0);
       double dyn = Ab[oXd] * vX;
-      const double d1 = dyn + Ab[oHd] * P[oXSp - 12];
-      const double d2 = d1 + Ab[oH6] * P[oXSp6 - 12];
+      const int zP = (int)((lds_cd*)sh.zero - P);  // stage 0 has no X_0 term: read zeros, not slot -1
+      const double d1 = dyn + Ab[oHd] * P[hp ? oXSp - 12 : zP];
+      const double d2 = d1 + Ab[oH6] * P[hp ? oXSp6 - 12 : zP];
       dyn = hp ? (isv ? d1 : d2) : dyn;
       dyn = isv ? dyn + bfx : dyn;
       const double q0 = qbc<0>(vf), q1 = qbc<1>(vf), q2 = qbc<2>(vf);
@@ -1167,6 +1200,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
         ndy = fmax(ndy, fabs(E[j] * dyp[j]));
         ineq += hj * fmax(dyp[j], 0.0) + lj * fmin(dyp[j], 0.0);
       }
+      if (phantom) ineq = 0.0;  // a sum: stage N-1 counts once
       double q3[2] = {0.0, 0.0};
       if (cl) {
         const double dif = 1.0 / Df, diX = 1.0 / DX;
@@ -1417,31 +1451,31 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 #pragma unroll
           for (int j = 0; j < 3; ++j) Ex[48 * k + 3 * s + j] = et[j];
           sync_all();
-          if (cl) {  // own columns: E_row A D_col
+          if (cl && !phantom) {  // own columns: E_row A D_col (in place: phantom rows keep out)
             const double dA = dyn_E(k, 6 + cc);
-            sh.Ab[fo] = dA * sh.Ab[fo] * dtf;
+            AbW[fo] = dA * AbW[fo] * dtf;
 #pragma unroll
-            for (int j = 0; j < 3; ++j) sh.Ab[fo + 1 + j] = dyn_E(k, 9 + j) * sh.Ab[fo + 1 + j] * dtf;
-            sh.Ab[fo + 4] = et[1] * sh.Ab[fo + 4] * dtf;
+            for (int j = 0; j < 3; ++j) AbW[fo + 1 + j] = dyn_E(k, 9 + j) * AbW[fo + 1 + j] * dtf;
+            AbW[fo + 4] = et[1] * AbW[fo + 4] * dtf;
             if (cc < 2) {
-              sh.Ab[fo + 5] = fr_E(k, f, 2 * cc) * sh.Ab[fo + 5] * dtf;
-              sh.Ab[fo + 6] = fr_E(k, f, 2 * cc + 1) * sh.Ab[fo + 6] * dtf;
+              AbW[fo + 5] = fr_E(k, f, 2 * cc) * AbW[fo + 5] * dtf;
+              AbW[fo + 6] = fr_E(k, f, 2 * cc + 1) * AbW[fo + 6] * dtf;
             } else {
 #pragma unroll
-              for (int t_ = 0; t_ < 5; ++t_) sh.Ab[fo + 5 + t_] = fr_E(k, f, t_) * sh.Ab[fo + 5 + t_] * dtf;
+              for (int t_ = 0; t_ < 5; ++t_) AbW[fo + 5 + t_] = fr_E(k, f, t_) * AbW[fo + 5 + t_] * dtf;
             }
-            sh.Ab[xo] = et[0] * sh.Ab[xo] * dtx;
+            AbW[xo] = et[0] * AbW[xo] * dtx;
             if (k < N - 1) {
               if (ph >= 6) {
-                sh.Ab[xo + 1] = dyn_E(k + 1, ph - 6) * sh.Ab[xo + 1] * dtx;
-                sh.Ab[xo + 2] = dyn_E(k + 1, ph) * sh.Ab[xo + 2] * dtx;
+                AbW[xo + 1] = dyn_E(k + 1, ph - 6) * AbW[xo + 1] * dtx;
+                AbW[xo + 2] = dyn_E(k + 1, ph) * AbW[xo + 2] * dtx;
               } else {
-                sh.Ab[xo + 1] = dyn_E(k + 1, ph) * sh.Ab[xo + 1] * dtx;
+                AbW[xo + 1] = dyn_E(k + 1, ph) * AbW[xo + 1] * dtx;
               }
             }
           }
           // cost scaling: c = 1 / max(mean |P|, 1)  (q = 0)
-          double ps = cl ? fabs(Pf) + fabs(PX) : 0.0;
+          double ps = cl && !phantom ? fabs(Pf) + fabs(PX) : 0.0;
           ps = wave_sum(ps);
           if ((t & 63) == 0) sh.red[wv] = ps;
           sync_all();
@@ -1597,7 +1631,17 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               g[2 * i + 1] = v.y;
             }
           };
-          if (t < 64) row12(Mb + GS);
+          // the rows of step j (j a constant after unrolling): every lane reads a slot the
+          // factorisation wrote -- the steps a chain does not take (half 1's first step,
+          // the bottom chain's steps past its BOT stages at even N) re-read a row of the
+          // chain's own, and their products are discarded by the hand-off select / the sink
+          auto rowp = [&](int j) __attribute__((always_inline)) -> swp* {
+            if (j >= 2 && j <= BOT) return Mb + GS * j;
+            const int jj = half == 0 ? (cr == 0 ? j : (j < BOT ? j : BOT))
+                                     : (cr == 0 ? (j > 2 ? j : 2) : (j < BOT + 1 ? j : BOT + 1));
+            return Mb + GS * jj;
+          };
+          if (t < 64) row12(rowp(1));
           sync_all();
           STAMP(3);
           if (t < 64) {
@@ -1606,12 +1650,12 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
             // instance's stage-parallel phases
             __builtin_amdgcn_s_setprio(3);
             // right-hand side of step j: top stage j (slot j), bottom stage N-1-j (slot
-            // MID+1+j, except the meeting stage MID at the bottom's last step MID-1, slot
-            // MID); na, nb at +12N, +24N
+            // MID+1+j, except the meeting stage MID at the bottom's last step BOT, slot
+            // MID, which the bottom re-reads in the steps it does not take); na at +12N
             lds_cd* const Bb = (lds_cd*)&sh.u.it.bo[0][0] + (12 * (cr == 0 ? 0 : MID + 1) + rr_);
             lds_cd* const Bm = (lds_cd*)&sh.u.it.bo[MID][rr_];
             auto rhs = [&](int j) __attribute__((always_inline)) -> lds_cd* {  // j: a constant
-              return (j == MID - 1 && cr != 0) ? Bm : Bb + 12 * j;
+              return (j >= BOT && cr != 0) ? Bm : Bb + 12 * j;
             };
             // w of stage kk(j-2) (half 1): top slot j-2, bottom slot MID-1+j; the other
             // lanes store into the sink with the same stride
@@ -1642,9 +1686,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               for (int i = 0; i < 12; ++i) gc[i] = g[i];
               const double bc = j <= MID ? bcn : 0.0;
               if (j < MID) {  // prefetch the next step's rows
-                row12(Mb + GS * (j + 1));
+                row12(rowp(j + 1));
               } else if (j == MID) {  // the meeting step: M^{-1} rows (half 0), the S walk (half 1)
-                row12(half == 0 ? GHs + RS * rr_ : Mb + GS * (MID + 1));
+                row12(half == 0 ? GHs + RS * rr_ : rowp(MID + 1));
                 lds_cd* qb = (lds_cd*)&sh.u.it.bo[MID][rr_];
                 b0 = qb[0]; b1 = qb[12 * N];
               } else {  // the last step: the first outward step's columns
@@ -1665,13 +1709,14 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               }
               if (j >= 2 && j <= MID) {  // half 1: w of stage kk(j-2)
                 Yb[12 * j] = acc;
-              } else if (j == MID + 1) {  // the meeting stage itself has no w (bottom)
-                *(cr == 0 ? Yb + 12 * j : sink) = acc;
+              } else if (j == MID + 1) {  // even N: the bottom's kk(MID-1) is the meeting stage (no w)
+                if constexpr (N & 1) Yb[12 * j] = acc;
+                else *(cr == 0 ? Yb + 12 * j : sink) = acc;
               }
               if (j <= MID) {
-                // half 0 continues with y_kk(j) (the bottom's step MID is idle), half 1
+                // half 0 continues with y_kk(j) (the bottom chain stops after step BOT), half 1
                 // receives y_kk(j-1) from half 0
-                const bool adv = j < MID || cr == 0;
+                const bool adv = j <= BOT || cr == 0;
                 src = keep_lo_take_lo(adv ? acc : src, src);
               } else {
                 xp = acc;
@@ -1702,14 +1747,18 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
               if (j < MID) {
 #pragma unroll
                 for (int i = 0; i < 12; ++i) g[i] = Ob[RS * i + GS * (MID - j - 1)];
-                bq = Wb[12 * (MID - j - 1)];
+                // (even N: the bottom chain has no step MID; it re-reads its last w)
+                if (j + 1 <= BOT) bq = Wb[12 * (MID - j - 1)];
+                else bq = Wb[12 * (MID - (cr == 0 ? j + 1 : BOT))];
               }
               asm volatile("" : : : "memory");
               const double acc = bdot12(gc, xp, bc);  // x = w - G' x_next with -G stored
               if (j < MID) {
                 xp = acc;
                 Xb[12 * (MID - j)] = acc;
-              } else {
+              } else if constexpr (N & 1) {
+                *Xb = acc;
+              } else {  // even N: the bottom chain has no step MID
                 *(cr == 0 ? Xb : sinkO) = acc;
               }
             }
@@ -1739,7 +1788,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           const double cFb = Ab[oFb], cFa = Ab[oFa], cF4 = Ab[oF4], cSw = op ? op->cf[4] : Ab[oF + 4];
           sync_all();
           STAMP(7);
-          const double xa = XSr[rXSp], xb = XSr[rXSp6];
+          const double xa = XSr[rXSpm], xb = XSr[rXSp6m];  // (stage 0: X_0 = 0, a zero slot)
           sX = XSr[rXS];
           asm volatile("" : : : "memory");
           {
@@ -1907,8 +1956,9 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
           constexpr double kPolishRho = 1e3;
           // the refinement contracts by the error of the explicit stage inverses, which
           // grows with the chain length: 10 steps land within 2e-10 of x* up to N = 32,
-          // N = 48 needs 20 (measured: 10 -> 2-4e-7, 20 -> 1e-10, tools/attic/polish48b.py)
-          constexpr int kPolishMinIter = N > 32 ? 20 : 10;
+          // N = 48 needs 20 (measured: 10 -> 2-4e-7, 20 -> 1e-10, tools/attic/polish48b.py),
+          // N = 64 more than 20 (20 -> 3.2e-8 on the fixtures, r03b)
+          constexpr int kPolishMinIter = N > 48 ? 30 : (N > 32 ? 20 : 10);
           const double a_pri = pri_res, a_dua = dua_res;
           const double axf = xf, axX = xX;
           double az[3], ay[3], zs[3], ys[3], bred[3], prho[3];
@@ -2104,7 +2154,7 @@ __global__ __launch_bounds__(16 * N, 2) void engine_kernel(mpcq_params p, Launch
 template <int N>
 hipError_t launch_t(bool fused, bool solve, const mpcq_params& p, const LaunchArgs& a,
                     hipStream_t s) {
-  const dim3 grid((unsigned)a.batch), block(16 * N);
+  const dim3 grid((unsigned)a.batch), block(16 * kRows<N>);
   if (kBig<N> && solve && !a.work) return hipErrorInvalidValue;  // the caller sizes it with work_doubles(N)
   // polish lives in its own instantiation: the production kernel's code (and its
   // register allocation in the ADMM loop) does not carry it
@@ -2124,11 +2174,11 @@ hipError_t launch_t(bool fused, bool solve, const mpcq_params& p, const LaunchAr
 #ifndef MPCQ_ENGINE_N
 #error "compile mpcq_engine.hip with -DMPCQ_ENGINE_N=<horizon> (see the Makefile)"
 #endif
-static_assert(MPCQ_ENGINE_N % 4 == 0 && MPCQ_ENGINE_N >= 4, "a wave64 holds four 16-lane stage rows");
+static_assert(MPCQ_ENGINE_N >= 4 && kRows<MPCQ_ENGINE_N> <= 64, "horizons 4..64 (1024 threads at most)");
 static_assert(sizeof(Smem<MPCQ_ENGINE_N>) <= 160 * 1024, "Smem<N> exceeds the CU's LDS");
 static_assert(Work<MPCQ_ENGINE_N>::SIZE == (kBig<MPCQ_ENGINE_N> ? work_doubles(MPCQ_ENGINE_N) : 72 + Work<MPCQ_ENGINE_N>::ZERO),
               "work_doubles(N) (mpcq_internal.h) and Work<N> disagree");
-static_assert(MPCQ_ENGINE_N > 16 || sizeof(Smem<MPCQ_ENGINE_N>) <= 80 * 1024,
+static_assert(kRows<MPCQ_ENGINE_N> > 16 || sizeof(Smem<MPCQ_ENGINE_N>) <= 80 * 1024,
               "Smem<N> must fit twice in a CU for N <= 16");
 
 #define MPCQ_CAT_(a, b) a##b

@@ -36,9 +36,12 @@ struct LaunchArgs {
 };
 
 // Doubles of engine workspace per instance: 0 up to 32 stages (everything in LDS);
-// beyond, a 288-double pad, S^{-1} (N x 144 + 2), F W (N x 72), R^{-1} Q (N x 36)
-// and a zero block (72)
-constexpr int64_t work_doubles(int N) { return N > 32 ? 288 + (int64_t)N * (144 + 72 + 36) + 2 + 72 : 0; }
+// beyond, a 288-double pad, S^{-1} (N x 144 + 2), F W (N x 72), R^{-1} Q (N x 36),
+// a zero block (72) and, beyond 56 stages, the scaled constraint values (126 N - 18,
+// rounded up to even)
+constexpr int64_t work_doubles(int N) {
+  return N > 32 ? 288 + (int64_t)N * (144 + 72 + 36) + 2 + 72 + (N > 56 ? ((126 * N - 18 + 1) & ~1) : 0) : 0;
+}
 
 // Planner launch (mpcq_planner.hip); layouts in include/mpcq.h (mpcq_plan_batch).
 struct PlanArgs {
@@ -94,7 +97,11 @@ hipError_t launch_order(const int32_t* iters, int64_t batch, int32_t* order, hip
 hipError_t launch_formulate(int N, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);
 hipError_t launch_solve(int N, bool fused, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);
 // the horizons the engine is compiled for (mpcq_dispatch.cpp, Makefile)
-#define MPCQ_HORIZONS(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(48)
+#define MPCQ_HORIZONS(X)                                                                                     \
+  X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22)  \
+  X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(33) X(34) X(35) X(36) X(37) X(38) X(39) X(40)  \
+  X(41) X(42) X(43) X(44) X(45) X(46) X(47) X(48) X(49) X(50) X(51) X(52) X(53) X(54) X(55) X(56) X(57) X(58)  \
+  X(59) X(60) X(61) X(62) X(63) X(64)
 bool horizon_supported(int N);
 int supported_horizons(int32_t* out, int cap);
 

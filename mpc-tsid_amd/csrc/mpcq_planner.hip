@@ -7,7 +7,8 @@
 //   roll               FootstepPlanner.py:401-425   lane-parallel row shift in LDS
 //   compute_footsteps  FootstepPlanner.py:284-361   lane c < 12 walks column c of
 //                                                   fsteps over the phases
-//   getRefStates       FootstepPlanner.py:76-159    lane j <= N owns xref column j
+//   getRefStates       FootstepPlanner.py:76-159    lane j owns xref column j (and
+//                                                   column j + 64 for N = 64)
 //
 // Rounding follows numpy's evaluation order exactly (the oracle
 // oracle/planner_oracle.c does the same and matches the reference bit for
@@ -26,7 +27,7 @@ namespace {
 struct PlanShared {
   alignas(16) double gait[100];
   alignas(16) double fs[260];
-  double v6[64], v7[64];  // xref columns 1..N (N <= 63: one lane per column)
+  double v6[128], v7[128];  // xref columns 1..N (lane j: columns j and j + 64)
   // per phase i of compute_footsteps: cos / sin of the yaw at the phase start and
   // the displacement dx, dy (FootstepPlanner.py:329-343), one lane per phase
   double ph_c[20], ph_s[20], ph_dx[20], ph_dy[20];
@@ -223,33 +224,26 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
 
   // ---- getRefStates (FootstepPlanner.py:76-159)
   if (a.ops & MPCQ_PLAN_REFSTATES) {
-    const int j = lane;
     const double Tg = pp.T_gait, dt = pp.dt;
-    if (col && j >= 1) {
-      const double yaw = linspace_at(0.0, Tg - dt, N, j - 1) * vr[5];
-      const double c = cos(yaw), s = sin(yaw);
-      x[6] = vr[0] * c - vr[1] * s;
-      x[7] = vr[0] * s + vr[1] * c;
-      sh.v6[j] = x[6];
-      sh.v7[j] = x[7];
-    }
-    __syncthreads();
-    if (col && j >= 1) {
-      double a0 = 0.0, a1 = 0.0;  // np.cumsum: left to right
-      for (int i = 1; i <= j; ++i) {
-        a0 += sh.v6[i];
-        a1 += sh.v7[i];
-      }
-      x[0] = dt * a0 + st[0];
-      x[1] = dt * a1 + st[1];
-      if (a.k == 0) x[2] = pp.h_ref;
-      x[5] = vr[5] * linspace_at(dt, Tg, N, j - 1);
-      x[11] = vr[5];
-    }
-    if (j == 0) {
+    // a second column per lane only when N + 1 > 64 (N = 64: column 64 on lane 0)
+    const int j2 = lane + 64;
+    const bool col2 = do_ref && j2 < NP;
+    double x2[12];
 #pragma unroll
-      for (int r = 0; r < 12; ++r) x[r] = st[r];
-    }
+    for (int r = 0; r < 12; ++r) x2[r] = col2 ? gx[r * NP + j2] : 0.0;
+    auto velocities = [&](int j, bool on, double (&xx)[12]) __attribute__((always_inline)) {
+      if (on && j >= 1) {
+        const double yaw = linspace_at(0.0, Tg - dt, N, j - 1) * vr[5];
+        const double c = cos(yaw), s = sin(yaw);
+        xx[6] = vr[0] * c - vr[1] * s;
+        xx[7] = vr[0] * s + vr[1] * c;
+        sh.v6[j] = xx[6];
+        sh.v7[j] = xx[7];
+      }
+    };
+    velocities(lane, col, x);
+    velocities(j2, col2, x2);
+    __syncthreads();
     // height / rotation command state machine (uniform per instance)
     int flag = sh.flag;
     double h_rot = sh.in[37];
@@ -266,22 +260,42 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
     } else if (flag == 0) {
       branch = 3;
     }
-    if (col && j >= 1) {
-      if (branch == 1) { x[2] = h_rot; x[8] = v2; }
-      else if (branch == 2) { x[8] = 0.0; x[9] = 0.0; x[10] = 0.0; }
-      else if (branch == 3) { x[2] = pp.h_ref; x[8] = 0.0; }
-      if (flag != 0) {
-        const double to = linspace_at(0.0, Tg - dt, N, j - 1);
-        x[3] = st[3] + vr[3] * to;  // xref[3, 0] was just set to abg[0]
-        x[4] = st[4] + vr[4] * to;
-        x[9] = vr[3];
-        x[10] = vr[4];
+    auto column = [&](int j, bool on, double (&xx)[12]) __attribute__((always_inline)) {
+      if (on && j >= 1) {
+        double a0 = 0.0, a1 = 0.0;  // np.cumsum: left to right
+        for (int i = 1; i <= j; ++i) {
+          a0 += sh.v6[i];
+          a1 += sh.v7[i];
+        }
+        xx[0] = dt * a0 + st[0];
+        xx[1] = dt * a1 + st[1];
+        if (a.k == 0) xx[2] = pp.h_ref;
+        xx[5] = vr[5] * linspace_at(dt, Tg, N, j - 1);
+        xx[11] = vr[5];
       }
-    }
-    if (col) {
+      if (j == 0) {
 #pragma unroll
-      for (int r = 0; r < 12; ++r) gx[r * NP + j] = x[r];
-    }
+        for (int r = 0; r < 12; ++r) xx[r] = st[r];
+      }
+      if (on && j >= 1) {
+        if (branch == 1) { xx[2] = h_rot; xx[8] = v2; }
+        else if (branch == 2) { xx[8] = 0.0; xx[9] = 0.0; xx[10] = 0.0; }
+        else if (branch == 3) { xx[2] = pp.h_ref; xx[8] = 0.0; }
+        if (flag != 0) {
+          const double to = linspace_at(0.0, Tg - dt, N, j - 1);
+          xx[3] = st[3] + vr[3] * to;  // xref[3, 0] was just set to abg[0]
+          xx[4] = st[4] + vr[4] * to;
+          xx[9] = vr[3];
+          xx[10] = vr[4];
+        }
+      }
+      if (on) {
+#pragma unroll
+        for (int r = 0; r < 12; ++r) gx[r * NP + j] = xx[r];
+      }
+    };
+    column(lane, col, x);
+    column(j2, col2, x2);
     if (lane == 0) {
       a.rot_flag[b] = flag;
       a.h_rot[b] = h_rot;
@@ -294,7 +308,7 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
 
 hipError_t launch_plan(const mpcq_planner_params& pp, const PlanArgs& a, hipStream_t s) {
   if (a.batch <= 0) return hipSuccess;
-  if (a.N < 1 || a.N + 1 > 64) return hipErrorInvalidValue;
+  if (a.N < 1 || a.N > 64) return hipErrorInvalidValue;
   hipLaunchKernelGGL(planner_kernel, dim3((unsigned)a.batch), dim3(64), 0, s, pp, a);
   return hipGetLastError();
 }

@@ -104,3 +104,8 @@ def retrieve_bytes_per_instance(N: int) -> int:
     rd = 8 * 24 * N + 8 * 12 * (N + 1) + 4 + 4 + 8 * 26 + 8 + 48
     wr = 8 * 12 * N + 8 * 24 * N + 8 * 13 + 48 + 96 + 96
     return rd + wr
+
+
+def polish_min_refinements(N: int) -> int:
+    """The engine's floor on polish refinement steps (mpcq_engine.hip kPolishMinIter)."""
+    return 30 if N > 48 else (20 if N > 32 else 10)

@@ -58,15 +58,17 @@ def gait_table(gait: str, n_steps: int) -> np.ndarray:
         g[0, 0] = n_steps
         g[0, 1:] = 1.0
         return g
-    if n_steps % 2 or n_steps < 4:
+    if n_steps < 4:
         raise ValueError(f"horizon {n_steps}: a gait period is two half periods of >= 2 steps")
-    half = period_steps(n_steps) // 2
-    n_periods = n_steps // (2 * half)
+    per = period_steps(n_steps)
+    n_periods = n_steps // per
     if n_periods > 4:
         raise ValueError(f"horizon {n_steps}: {n_periods} periods do not fit the 20-row table")
+    # an odd single-period horizon has half periods of floor(N/2) and ceil(N/2) steps
+    h1, h2 = per // 2, per - per // 2
     masks = GAIT_MASKS[gait]
     for i in range(n_periods):
-        g[4 * i:4 * i + 4, 0] = (1, half - 1, 1, half - 1)
+        g[4 * i:4 * i + 4, 0] = (1, h1 - 1, 1, h2 - 1)
         for r in range(4):
             g[4 * i + r, 1:] = masks[r]
     return g

@@ -52,7 +52,7 @@ void oracle_retrieve(const mpcq_params* p, int N, const double* x, const double*
                      const double* fsteps, const double* gait, const double* shoulders, int failed,
                      double* x_robot, double* q_w, double* cost, double* warm_x, double* next_state,
                      double* next_l_feet) {
-  if (N < 1 || N > 64) return;  /* the planner's horizons (N <= 63) */
+  if (N < 1 || N > 64) return;  /* the engine's horizons (N <= 64) */
   const int NP = N + 1, n = 24 * N;
   for (int r = 0; r < 12; ++r)
     for (int k = 0; k < N; ++k) x_robot[r * N + k] = x[12 * k + r] + xref[r * NP + k + 1];

@@ -41,10 +41,17 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def golden_h():
-    """Fixtures at the other horizons (gen_golden.py horizons): {N: {field: array}}."""
-    d = np.load(os.path.join(GOLDEN, "golden_horizons.npz"))
+    """Fixtures at the other horizons (gen_golden.py horizons / horizons_r3):
+    {N: {field: array}}."""
     out = {}
-    for N in d["horizons"]:
-        pre = f"n{int(N)}_"
-        out[int(N)] = {k[len(pre):]: d[k] for k in d.files if k.startswith(pre)}
+    for name in ("golden_horizons.npz", "golden_horizons_r3.npz"):
+        d = np.load(os.path.join(GOLDEN, name))
+        for N in d["horizons"]:
+            pre = f"n{int(N)}_"
+            out[int(N)] = {k[len(pre):]: d[k] for k in d.files if k.startswith(pre)}
     return out
+
+
+# the horizons the fixtures cover besides 16 / 32: multiples of 4 up to 32, N = 48
+# (round 2), and round 3's non-multiples of 4, odd N and the range up to 64
+FIXTURE_HORIZONS = (4, 5, 6, 8, 10, 12, 13, 20, 24, 28, 33, 36, 40, 48, 57, 64)

@@ -3,6 +3,8 @@
     python tests/golden/gen_golden.py            # writes tests/golden/golden_n16.npz, golden_n32.npz
     python tests/golden/gen_golden.py horizons   # writes tests/golden/golden_horizons.npz
                                                  # (N = 4, 8, 12, 20, 24, 28 and 48; keys n<N>_<field>)
+    python tests/golden/gen_golden.py horizons_r3  # golden_horizons_r3.npz: N = 5, 6, 10, 13, 33,
+                                                   # 36, 40, 57, 64
 
 What it does, per instance:
 1. Inputs: seeded synthetic (xref, fsteps) from mpcq.synth (trot / bound /
@@ -267,6 +269,11 @@ def build(N: int, per_gait: int, seed: int, extra=True):
 
 
 HORIZONS = ((4, 2, 404), (8, 4, 808), (12, 2, 1212), (20, 2, 2020), (24, 4, 2424), (28, 2, 2828), (48, 1, 4848))
+# round 3: horizons that are not a multiple of 4 (phantom stage rows), odd ones (the
+# two sweep chains equally long) and the global-workspace range up to n_periods = 4
+# (N = 64; beyond 56 stages the constraint values leave LDS too)
+HORIZONS_R3 = ((5, 1, 505), (6, 2, 606), (10, 2, 1010), (13, 1, 1313), (33, 1, 3333), (36, 1, 3636), (40, 1, 4040),
+               (57, 1, 5757), (64, 1, 6464))
 
 
 def main_horizons():
@@ -282,9 +289,24 @@ def main_horizons():
     print("wrote", path, os.path.getsize(path), "bytes")
 
 
+def main_horizons_r3():
+    """golden_horizons_r3.npz: HORIZONS_R3, same fields and key scheme as main_horizons."""
+    out = {}
+    for N, per_gait, seed in HORIZONS_R3:
+        arrs = build(N, per_gait, seed)
+        for k, v in arrs.items():
+            out[f"n{N}_{k}"] = v
+    path = os.path.join(HERE, "golden_horizons_r3.npz")
+    np.savez_compressed(path, horizons=np.array([h[0] for h in HORIZONS_R3]), **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "horizons":
         main_horizons()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "horizons_r3":
+        main_horizons_r3()
         return
     for N, per_gait, seed in ((16, 16, 1234), (32, 4, 4321)):
         arrs = build(N, per_gait, seed)

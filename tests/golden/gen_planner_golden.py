@@ -147,9 +147,10 @@ def main():
             N, out = run_scenario(FP, kind, n_periods, seed=5000 + sid)
             sid += 1
             groups.setdefault(N, []).append((kind, out))
-    # other horizons: dt = 0.04 (N = 8 per period: n_periods 1 and 3 -> N = 8, 24) and
-    # three periods at dt = 0.02 (N = 48); keys n<N>_*, the N = 16 / 32 ones unchanged
-    for dt, n_periods in ((0.04, 1), (0.04, 3), (0.02, 3)):
+    # other horizons: dt = 0.04 (N = 8 per period: n_periods 1 and 3 -> N = 8, 24),
+    # three and (round 3) four periods at dt = 0.02 (N = 48, 64); keys n<N>_*, the
+    # N = 16 / 32 ones unchanged
+    for dt, n_periods in ((0.04, 1), (0.04, 3), (0.02, 3), (0.02, 4)):
         for kind in ("trot", "bound", "random", "static"):
             N, out = run_scenario(FP, kind, n_periods, seed=7000 + sid, dt=dt)
             sid += 1

@@ -25,7 +25,7 @@ def mpcq():
 
 @pytest.fixture(scope="module")
 def engines(mpcq):
-    es = {N: mpcq.Engine(N) for N in (8, 16, 24, 32, 48)}
+    es = {N: mpcq.Engine(N) for N in (8, 10, 16, 24, 32, 48, 64)}
     yield es
     for e in es.values():
         e.close()
@@ -53,7 +53,7 @@ def _close(a, b, tol=PLAN_TOL):
     return float(d.max(initial=0)), float((d == 0).mean())
 
 
-@pytest.mark.parametrize("N", [8, 16, 24, 32, 48])
+@pytest.mark.parametrize("N", [8, 16, 24, 32, 48, 64])
 def test_planner_vs_reference_fixtures(mpcq, engines, N):
     """Every scenario of planner_golden.npz runs as one instance of a batch,
     tick by tick as processing.py:81-131 drives the reference."""
@@ -89,7 +89,7 @@ def _random_batch(rng, B, N):
         if r < 0.6:
             gait[b] = synth.gait_table(kinds[b % 3], N)
         elif r < 0.95:  # random phases summing to N, random masks
-            nph = int(rng.integers(1, 12))
+            nph = int(rng.integers(1, min(12, N)))
             cuts = np.sort(rng.choice(np.arange(1, N), nph - 1, replace=False)) if nph > 1 else np.array([], int)
             d = np.diff(np.concatenate([[0], cuts, [N]]))
             gait[b, :nph, 0] = d
@@ -108,7 +108,7 @@ def _random_batch(rng, B, N):
     return gait, state, l_feet, v_ref, reduced
 
 
-@pytest.mark.parametrize("N", [16, 32])
+@pytest.mark.parametrize("N", [10, 16, 32, 64])
 def test_planner_vs_oracle_random(mpcq, engines, N):
     from oracle import oracle as O
     rng = np.random.default_rng(77 + N)

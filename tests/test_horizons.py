@@ -1,14 +1,15 @@
-"""CPU: the oracle at every horizon the engine compiles (N = 4j <= 32) and at
-N = 48 (n_periods = 3), pinned to fixtures captured from the unmodified
-reference MPC.py (tests/golden/gen_golden.py horizons): the CSC pattern, the
+"""CPU: the oracle at the fixture horizons (N = 4j <= 32, N = 48 = n_periods 3;
+round 3: N = 5, 6, 10, 13, 33, 36, 40, 57 and 64 = n_periods 4), pinned to
+fixtures captured from the unmodified reference MPC.py (tests/golden/gen_golden.py
+horizons / horizons_r3): the CSC pattern, the
 A / l / u handed to OSQP in both modes, and the polished solve on the certified
 optimum x*.  The reference takes any n_steps (MPC.py:22-26; FootstepPlanner.py:55
 n_steps = n_periods T_gait / dt)."""
 import numpy as np
 import pytest
+from conftest import FIXTURE_HORIZONS as HORIZONS
 
 FORM_TOL = 1e-14
-HORIZONS = (4, 8, 12, 20, 24, 28, 48)
 
 
 def _rel(a, b):

@@ -40,7 +40,7 @@ def _same(a, b, tol):
     return np.array_equal(np.isnan(a), np.isnan(b)) and np.nanmax(np.abs(a - b), initial=0.0) <= tol
 
 
-@pytest.mark.parametrize("N", [8, 16, 24, 32, 48])
+@pytest.mark.parametrize("N", [8, 16, 24, 32, 48, 64])
 def test_planner_oracle_bit_exact(gold, N):
     """Bit-identical at N <= 32.  At N = 48 numpy's vectorised sin / cos (arrays of 48
     yaw values, angles up to ~1 rad) and the host libm differ by an ulp on a few

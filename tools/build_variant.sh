@@ -12,11 +12,15 @@ NAME=$1; SRC=$(realpath "$2"); shift 2
 OUT=$C/build/variants; mkdir -p $OUT/$NAME
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -I$C"
 HS=${VARIANT_HORIZONS:-16 32}  # the horizons compiled from the variant source
-for n in $HS; do /opt/rocm/bin/hipcc $F "$@" -DMPCQ_ENGINE_N=$n -c -o $OUT/$NAME/e$n.o -x hip $SRC & done
+J=0
+for n in $HS; do
+  /opt/rocm/bin/hipcc $F "$@" -DMPCQ_ENGINE_N=$n -c -o $OUT/$NAME/e$n.o -x hip $SRC &
+  J=$((J + 1)); if [ $((J % 8)) -eq 0 ]; then wait; fi
+done
 wait
 # the other horizons from the production objects
 OBJS=""
-for n in 4 8 12 16 20 24 28 32 48; do
+for n in $(seq 4 64); do
   if [[ " $HS " == *" $n "* ]]; then OBJS="$OBJS $OUT/$NAME/e$n.o"; else OBJS="$OBJS $C/build/engine_n$n.o"; fi
 done
 /opt/rocm/bin/hipcc $F -shared -o $OUT/libmpcq_$NAME.so $OBJS $C/build/mpcq_planner.o $C/build/mpcq_session.o \

@@ -1850,9 +1850,12 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             __attribute__((always_inline)) {
           constexpr bool DELTA = decltype(delta_tag)::value;
           double uf, beta, sf, sX, ax[3];
-          ph_rhs(true, &ops, kNoW, 0.0, 0.0, uf, beta);
+          // (beyond 32 stages the operands are read per iteration: held, they cost the
+          // register budget of the 9..16-wave workgroups -- N = 48: scratch 840 -> 712 B
+          // per lane, 17.68 -> 16.75 us per iteration, profiles/r03c_iterbench.txt)
+          ph_rhs(true, kBig<N> ? nullptr : &ops, kNoW, 0.0, 0.0, uf, beta);
           ph_sweep();
-          ph_recover(&ops, uf, beta, sf, sX, ax);
+          ph_recover(kBig<N> ? nullptr : &ops, uf, beta, sf, sX, ax);
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
             const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
@@ -1881,7 +1884,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // held in registers through the iterations up to the next check: no LDS traffic
           // for them in the loop
           RhsOps ops;
-          load_rhs_ops(ops);
+          if constexpr (!kBig<N>) load_rhs_ops(ops);
 #pragma nounroll
           for (int r_ = 1; r_ < until; ++r_, ++iter) admm_iter(std::false_type{}, ops, dyv, dxf_, dxX_);
           admm_iter(std::true_type{}, ops, dyv, dxf_, dxX_);

@@ -432,11 +432,13 @@ __host__ __device__ constexpr int SLOT(int q) { return GS * q + (q > N / 2 ? kSl
 // doubles per instance, L2-resident), the rest stays in LDS (N = 48: 140 KB).
 template <int N>
 constexpr bool kBig = N > 32;
-// Beyond 56 stages the scaled constraint values (126 N - 18 doubles) leave LDS as well
-// (N = 64: 185 KB with them, 121 KB without); the engine reads them through the
-// same accessors, the stage-parallel phases from L2.
+// F W stays in LDS at every N (the ADMM loop reads it every iteration: from L2 at
+// N = 48 it cost the right-hand-side phase ~14 k cycles per iteration, r03d
+// stamps); beyond 49 stages the scaled constraint values (126 N - 18 doubles) leave
+// LDS instead (N = 64: 197 KB with them, 133 KB without); the engine reads them
+// through the same accessors, the stage-parallel phases from L2.
 template <int N>
-constexpr bool kAbG = N > 56;
+constexpr bool kAbG = N > 49;
 template <int N>
 struct Work {  // offsets (doubles) inside one instance's workspace
   // SM starts two slots in (a pad kept from round 2; the sweep no longer reads it)
@@ -457,7 +459,7 @@ struct Smem {
   // (N > 32: these three live in the global workspace, Work<N>)
   alignas(16) double Sm[kBig<N> ? 1 : N][GS];  // S_k^{-1} / U_k^{-1} of stage k at SLOT(SIG(k)), row-major (row stride RS)
   double Smpad[2];
-  double FWs[kBig<N> ? 1 : N][72];  // F_k W_k (12x6, row psi at [6 psi]); W_k = B_k' R on rows 6..11
+  double FWs[N][72];  // F_k W_k (12x6, row psi at [6 psi]); W_k = B_k' R on rows 6..11
   double QL[kBig<N> ? 1 : N][36];   // B_k F_k W_k = R^{-1} W_k' F_k W_k (6x6)
   union {
     struct {
@@ -522,22 +524,22 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
   else AbW = sh.Ab;
   acd* Ab = (acd*)AbW;
   lds_cd* GHr = (lds_cd*)&sh.GH[0][0];
-  // S^{-1}, F W, R^{-1} Q: LDS, or (N > 32) this instance's global workspace
+  // S^{-1}, R^{-1} Q: LDS, or (N > 32) this instance's global workspace; F W: LDS
   using wcd = std::conditional_t<BIG, const double, lds_cd>;
   using wdd = std::conditional_t<BIG, double, lds_d>;
   wcd* SmR;
-  wcd* FWr;
+  lds_cd* FWr;
   wcd* QLr;
   wdd* SmW;
-  wdd* FWW;
+  lds_d* FWW;
   wdd* QLW;
   int zFW, zQL;  // offsets of a zero block from FWr / QLr (masked reads)
   if constexpr (BIG) {
     double* const wk = SOLVE ? a.work + b * Work<N>::SIZE : nullptr;  // (formulation only: unused)
     SmW = wk + Work<N>::SM;
-    FWW = wk + Work<N>::FW;
+    FWW = (lds_d*)&sh.FWs[0][0];  // (Work<N>::FW stays reserved, unused)
     QLW = wk + Work<N>::QL;
-    zFW = Work<N>::ZERO - Work<N>::FW;
+    zFW = (int)(sh.zero - &sh.FWs[0][0]);
     zQL = Work<N>::ZERO - Work<N>::QL;
     if (SOLVE && t < 72) wk[Work<N>::ZERO + t] = 0.0;
   } else {
@@ -548,7 +550,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     zQL = (int)(sh.zero - &sh.QL[0][0]);
   }
   SmR = (wcd*)SmW;
-  FWr = (wcd*)FWW;
+  FWr = (lds_cd*)FWW;
   QLr = (wcd*)QLW;
   double* const gh0 = &sh.GH[0][0];
   int fo = FO<N>(k, f, cc), xo = XO<N>(k, ph);  // own force / state column in Ab
@@ -1592,7 +1594,8 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // (the barrier that publishes bo / na / nb opens ph_sweep)
       };
       auto ph_sweep = [&]() __attribute__((always_inline)) {
-          // P5-P7: the state solve on wave 0 alone (no block barrier inside).
+          // P5-P7: the state solve on wave 0 alone (no block barrier inside; beyond 32
+          // stages one pair of barriers, see WPH).
           // Inward step j = 1..MID: top kk(j) = j, bottom kk(j) = N-1-j.  Half 0 (rows
           // 0 top / 1 bottom) runs the recurrence y_kk = b_kk - G_kk y_kk(j-1) (G_kk of
           // the top in GH[kk], H_kk of the bottom in GH[kk+1], stored negated), one
@@ -1614,14 +1617,21 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // top slot j-2 / bottom slot MID-1+j.  Step 1's rows are iteration-invariant:
           // wave 0 reads them before the barrier that publishes the right-hand sides.
           // (N > 32: S^{-1} is global, so the row pointer is a generic one)
-          using swp = std::conditional_t<BIG, const double, lds_cd>;
-          using swp2 = std::conditional_t<BIG, const dbl2, lds_cd2>;
-          swp* GHs;
-          if constexpr (BIG) GHs = (const double*)&sh.GH[0][0];
-          else GHs = GHr;
+          // WPH (beyond 32 stages, where S^{-1} lives in L2): the S^{-1} products leave the
+          // sweep -- half 0 stores each y_k, and between the inward and the outward sweep
+          // every stage row turns its own y_k into w_k = S_k^{-1} y_k (one L2 round trip
+          // for all stages, instead of one per inward step on the sweep wave); half 1
+          // then shadows half 0 (same LDS rows, results to the sink).
+          constexpr bool WPH = BIG;
+          const int hh = WPH ? 0 : half;  // the row walk a lane follows
+          using swp = lds_cd;
+          using swp2 = lds_cd2;
+          swp* const GHs = GHr;
           // (the bottom chain's slots are past N/2: +2, SLOT)
-          swp* const Mb = half == 0 ? GHs + (GS * (cr == 0 ? 0 : MID) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_)
-                                    : (swp*)SmR + (GS * (cr == 0 ? -2 : MID - 1) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_);
+          swp* Mb;
+          if constexpr (WPH) Mb = GHs + (GS * (cr == 0 ? 0 : MID) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_);
+          else Mb = half == 0 ? GHs + (GS * (cr == 0 ? 0 : MID) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_)
+                              : (swp*)SmR + (GS * (cr == 0 ? -2 : MID - 1) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_);
           double g[12];
           auto row12 = [&](swp* q) __attribute__((always_inline)) {  // 16-B aligned row: 6 ds_read_b128
 #pragma unroll
@@ -1637,13 +1647,17 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // chain's own, and their products are discarded by the hand-off select / the sink
           auto rowp = [&](int j) __attribute__((always_inline)) -> swp* {
             if (j >= 2 && j <= BOT) return Mb + GS * j;
-            const int jj = half == 0 ? (cr == 0 ? j : (j < BOT ? j : BOT))
-                                     : (cr == 0 ? (j > 2 ? j : 2) : (j < BOT + 1 ? j : BOT + 1));
+            const int jj = hh == 0 ? (cr == 0 ? j : (j < BOT ? j : BOT))
+                                   : (cr == 0 ? (j > 2 ? j : 2) : (j < BOT + 1 ? j : BOT + 1));
             return Mb + GS * jj;
           };
           if (t < 64) row12(rowp(1));
           sync_all();
           STAMP(3);
+          // outward step j reads G_{MID-j+1}' (top, slot MID+1-j) / H_{MID+j-1}'
+          // (bottom, slot N-j) columns: Ob + (MID - j) GS (LDS offsets are unsigned,
+          // so the bases sit at the lowest slot a chain reaches)
+          lds_cd* const Ob = GHr + (GS * (cr == 0 ? 1 : N - MID) + (cr == 0 ? 0 : kSlotPad<N>) + rr_);
           if (t < 64) {
             // the sweeps are every wave's critical path (the other waves of the
             // instance wait at the barrier): issue them ahead of a co-resident
@@ -1660,8 +1674,11 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             // w of stage kk(j-2) (half 1): top slot j-2, bottom slot MID-1+j; the other
             // lanes store into the sink with the same stride
             lds_d* const sink = (lds_d*)&sh.red[0] + (t & 31);
-            lds_d* const Yb = (half == 1 && s < 12) ? (lds_d*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? -2 : MID - 1) + rr_)
-                                                    : sink;
+            lds_d* const Yb = (!WPH && half == 1 && s < 12)
+                                  ? (lds_d*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? -2 : MID - 1) + rr_) : sink;
+            // WPH: y of step j's stage (top slot j, bottom slot MID+1+j: SIG) from half 0
+            lds_d* const Yh = (WPH && half == 0 && s < 12)
+                                  ? (lds_d*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? 0 : MID + 1) + rr_) : sink;
             // right-hand sides run two steps ahead: step j sums the one of step j+1
             // (loaded during step j-1) and loads the one of step j+2; half 1 (the w
             // products) starts its chain from 0.  The first two (y_kk(0) and step 1's)
@@ -1672,12 +1689,9 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             double c0 = rhs(1)[0], c1 = rhs(1)[12 * N];
             asm volatile("" : "+v"(s0), "+v"(s1), "+v"(c0), "+v"(c1));
             double src = half == 0 ? s0 + s1 : 0.0;  // y_kk(0) (half 0)
+            if constexpr (WPH) *Yh = src;
             double bcn = (c0 + c1) * m0;
             double b0 = rhs(2)[0], b1 = rhs(2)[12 * N];
-            // outward step j reads G_{MID-j+1}' (top, slot MID+1-j) / H_{MID+j-1}'
-            // (bottom, slot N-j) columns: Ob + (MID - j) GS (LDS offsets are unsigned,
-            // so the bases sit at the lowest slot a chain reaches)
-            lds_cd* const Ob = GHr + (GS * (cr == 0 ? 1 : N - MID) + (cr == 0 ? 0 : kSlotPad<N>) + rr_);
 #pragma unroll
             for (int j = 1; j <= MID + 1; ++j) {
               asm volatile("" : : : "memory");
@@ -1688,7 +1702,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               if (j < MID) {  // prefetch the next step's rows
                 row12(rowp(j + 1));
               } else if (j == MID) {  // the meeting step: M^{-1} rows (half 0), the S walk (half 1)
-                row12(half == 0 ? GHs + RS * rr_ : rowp(MID + 1));
+                row12(hh == 0 ? GHs + RS * rr_ : rowp(MID + 1));
                 lds_cd* qb = (lds_cd*)&sh.u.it.bo[MID][rr_];
                 b0 = qb[0]; b1 = qb[12 * N];
               } else {  // the last step: the first outward step's columns
@@ -1707,6 +1721,9 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               if (j + 2 <= MID) {
                 b0 = rhs(j + 2)[0]; b1 = rhs(j + 2)[12 * N];
               }
+              if constexpr (WPH) {  // y of stage kk(j) (the meeting stage's y_MID / v_MID stay in registers)
+                if (j < MID) *((cr == 0 || j < BOT) ? Yh + 12 * j : sink) = acc;
+              }
               if (j >= 2 && j <= MID) {  // half 1: w of stage kk(j-2)
                 Yb[12 * j] = acc;
               } else if (j == MID + 1) {  // even N: the bottom's kk(MID-1) is the meeting stage (no w)
@@ -1724,6 +1741,29 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               }
             }
             STAMP(6);
+          }
+          if constexpr (WPH) {
+            // w_k = S_k^{-1} y_k for every stage but the meeting one, stage-parallel: lane
+            // LN(ph) of stage k's row takes row ph of S_k^{-1} (L2) and y_k by row broadcast,
+            // the same products in the same order as the lagging half's (bit-identical)
+            sync_all();
+            using wcd2 = const dbl2;
+            const dbl2* const q = (wcd2*)(SmR + SLOT<N>(SIG<N>(k)) + RS * ph);
+            double srow[12];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+              const dbl2 v = q[i];
+              srow[2 * i] = v.x;
+              srow[2 * i + 1] = v.y;
+            }
+            double* const yk = &sh.u.it.yv[SIG<N>(k)][ph];
+            const double wk = bdot_ln12(srow, *yk, 0.0);
+            // in place: the row's reads of y_k precede (DPP operands); phantom rows keep out
+            // (stage N-1's row may sit in another wave and read y after their store)
+            if (cl && k != MID && !phantom) *yk = wk;
+            sync_all();
+          }
+          if (t < 64) {
             // Outward step j: top kk = MID-j: X_kk = w_kk - G_{kk+1}' X_{kk+1}; bottom
             // kk = MID+j: X_kk = w_kk - H_{kk-1}' X_{kk-1} (columns from Ob - j GS).  Lane
             // rr reads column rr (a full 12-term product per lane; half 1 repeats half 0).
@@ -1779,7 +1819,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
 #pragma unroll
           for (int i = 0; i < 3; ++i) {  // 16-B aligned pairs: ds_read_b128 (twice ds_read2_b64's LDS rate)
             using wcd2 = std::conditional_t<BIG, const dbl2, lds_cd2>;
-            const dbl2 fa = ((wcd2*)(FWr + oFW))[i], qa = ((wcd2*)(QLr + oQLm))[i];
+            const dbl2 fa = ((lds_cd2*)(FWr + oFW))[i], qa = ((wcd2*)(QLr + oQLm))[i];
             fwl[2 * i] = fa.x; fwl[2 * i + 1] = fa.y;
             qll[2 * i] = qa.x; qll[2 * i + 1] = qa.y;
           }

@@ -1,12 +1,16 @@
-# Every bench line of DESIGN.md §5 plus the rocprof passes, tagged: bash tools/bench_all.sh r02l
+# Every bench line of DESIGN.md §5 plus the rocprof passes, tagged: bash tools/bench_all.sh r03f
+# (the headline mode is OSQP as MPC.py configures it; each qp line carries the polish=2 companion)
 set -o pipefail
 T=${1:?tag}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
-timeout -k 10 240 python -u bench.py > $O/${T}_bench_c2.json 2> $O/${T}_bench_c2.err &&
-timeout -k 10 240 python -u bench.py --no-polish > $O/${T}_bench_c2_nopolish.json 2> $O/${T}_bench_c2_nopolish.err &&
-timeout -k 10 240 python -u bench.py --config c3 > $O/${T}_bench_c3.json 2> $O/${T}_bench_c3.err &&
+cd $R
+timeout -k 10 300 python -u bench.py > $O/${T}_bench_c2.json 2> $O/${T}_bench_c2.err &&
+timeout -k 10 300 python -u bench.py --config c3 > $O/${T}_bench_c3.json 2> $O/${T}_bench_c3.err &&
 timeout -k 10 240 python -u bench.py --config c1 > $O/${T}_bench_c1.json 2> $O/${T}_bench_c1.err &&
 timeout -k 10 300 python -u bench.py --config c4 --steps 3 --warmup 1 > $O/${T}_bench_c4_1gpu.json 2> $O/${T}_bench_c4.err &&
 timeout -k 10 300 python -u bench.py --config c5 --steps 3 --warmup 1 > $O/${T}_bench_c5_1gpu.json 2> $O/${T}_bench_c5.err &&
-bash tools/profile.sh $T
+timeout -k 10 300 python -u bench.py --mode tick --steps 20 --warmup 4 > $O/${T}_bench_tick_c2.json 2> $O/${T}_bench_tick_c2.err &&
+timeout -k 10 300 python -u bench.py --mode plan --cpu-sample 4096 > $O/${T}_bench_plan.json 2> $O/${T}_bench_plan.err &&
+bash tools/profile.sh $T --config c2 &&
+bash tools/profile.sh ${T}c3 --config c3

@@ -4,4 +4,5 @@ O=gpurun_out
 timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/r03e_pytest_gpu.log 2>&1 &&
 timeout -k 10 300 python -u tools/iterbench.py --N 48 --reps 3 > $O/r03e_iter48.txt 2>&1 &&
 timeout -k 10 300 python -u tools/iterbench.py --N 64 --reps 2 > $O/r03e_iter64.txt 2>&1 &&
+timeout -k 10 300 python -u tools/iterbench.py --N 32 --reps 3 > $O/r03e_iter32.txt 2>&1 &&
 MPCQ_LIB_VARIANT=exp:stamps48 timeout -k 10 300 python -u tools/stamps.py --N 48 --batch 256 --copies 2 > $O/r03e_stamps48.txt 2>&1

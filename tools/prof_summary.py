@@ -43,7 +43,7 @@ def mean(v):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--key", default="c2_N16_B1024_polish")
+    ap.add_argument("--key", default="c2_N16_B1024")
     ap.add_argument("--instances", type=int, default=1024)
     ap.add_argument("--kernel", default="engine_kernel", help="substring of the kernel the counters describe")
     a = ap.parse_args()

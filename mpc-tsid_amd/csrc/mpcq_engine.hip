@@ -174,6 +174,21 @@ __device__ __forceinline__ double bdot_ln12(const double (&g)[12], double v, dou
         "v"(g[8]), "v"(g[9]), "v"(g[10]), "v"(g[11]));
   return a0;
 }
+// i0 + sum_{j<6} g_j * v_j, v_j broadcast from lane j of the row: half of a
+// 12-term row product (the split sweep, ph_sweep)
+__device__ __forceinline__ double bdot6(const double (&g)[6], double v, double i0) {
+  double a0 = i0;
+  asm volatile("s_nop 1\n\t"
+      "v_fmac_f64_dpp %0, %1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %3 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %4 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %5 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %6 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %1, %7 row_newbcast:5 row_mask:0xf bank_mask:0xf"
+      : "+v"(a0)
+      : "v"(v), "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]), "v"(g[4]), "v"(g[5]));
+  return a0;
+}
 // i0 + sum_i g_i * v(lane LN(6 + i)), i < 6: the velocity slots
 __device__ __forceinline__ double bdot_ln6v(const double (&g)[6], double v, double i0) {
   double a0 = i0;
@@ -228,6 +243,16 @@ __device__ __forceinline__ double row_pair_sum(double v) {
   const long long b = __double_as_longlong(v);
   const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
   const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  const double a0 = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
+  const double a1 = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+  return a0 + a1;
+}
+// v(lane l) + v(lane l +- 32): rows 0 + 2 and rows 1 + 3 (one add of the same two values
+// in both lanes of a pair: the sum is bit-identical in both)
+__device__ __forceinline__ double pair_sum32(double v) {
+  const long long b = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
   const double a0 = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
   const double a1 = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
   return a0 + a1;
@@ -1593,9 +1618,193 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           }
           // (the barrier that publishes bo / na / nb opens ph_sweep)
       };
-      auto ph_sweep = [&]() __attribute__((always_inline)) {
-          // P5-P7: the state solve on wave 0 alone (no block barrier inside; beyond 32
-          // stages one pair of barriers, see WPH).
+      auto ph_sweep_split = [&]() __attribute__((always_inline)) {
+          // P5-P7: the state solve.  The two chains run on wave 0, each on a pair of rows
+          // that splits every 12-term row product in two: rows 0 / 1 (top / bottom chain)
+          // take the first six terms and the right-hand side, rows 2 / 3 the last six, and
+          // one permlane32 swap-add joins the halves (rows 0 + 2, 1 + 3).  Rows 2 / 3 hold
+          // the chain vector rotated by six lanes (row_ror:10), so both halves broadcast
+          // from lanes 0..5 with the same instruction.  Inward step j = 1..MID: y_kk =
+          // b_kk - G_kk y_kk(j-1) (top kk = j, G_kk in GH slot j; bottom kk = N-1-j, H_kk
+          // in slot MID+j, stopping after BOT steps), each y stored to its stage's yv slot;
+          // step MID+1: the meeting stage x_m = M^{-1} (y_m + v_m - b_m) (the two pairs
+          // joined by permlane16).  Then, on every wave, w_k = S_k^{-1} y_k stage-parallel
+          // (one barrier pair); then the outward steps x_kk = w_kk - G' x_next on wave 0.
+          // Used beyond 32 stages, where S^{-1} lives in L2 (N = 48: 13.9 -> 12.9 us per
+          // iteration); up to 32 stages ph_sweep_lag is faster (N = 16: 1.90 vs 2.31 us,
+          // N = 32: 3.31 vs 3.92, profiles/r03h_iterbench.txt): the split saves six FMAs and
+          // three row reads per step but adds the swap-add, the rotation and the selects,
+          // and the stage-parallel S^{-1} phase with its two barriers.
+          const int hi = (t >> 5) & 1;  // rows 2 / 3: the second six terms
+          const int h6 = 6 * hi;
+#ifndef MPCQ_REP_SWEEP
+#define MPCQ_REP_SWEEP 1
+#endif
+#pragma nounroll
+          for (int rep_ = 0; rep_ < MPCQ_REP_SWEEP; ++rep_) {  // > 1: timing experiments only
+          double xp = 0.0;
+          double g[6];
+          // lane rr of a row reads entries h6..h6+5 of row rr of the step's matrix
+          // (16-B aligned: 3 ds_read_b128); the bottom chain's slots sit past N/2 (+2, SLOT)
+          lds_cd* const Mb = GHr + (GS * (cr == 0 ? 0 : MID) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_ + h6);
+          auto row6 = [&](lds_cd* q) __attribute__((always_inline)) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+              const dbl2 v = ((lds_cd2*)q)[i];
+              g[2 * i] = v.x;
+              g[2 * i + 1] = v.y;
+            }
+          };
+          // step j's rows (j a constant after unrolling); the bottom chain's steps past BOT
+          // (even N) re-read its last matrix, their products discarded by the hand-off select
+          auto rowp = [&](int j) __attribute__((always_inline)) -> lds_cd* {
+            if (j <= BOT) return Mb + GS * j;
+            return Mb + GS * (cr == 0 ? j : BOT);
+          };
+          if (t < 64) row6(rowp(1));
+          sync_all();
+          STAMP(3);
+          // outward step j reads G_{MID-j+1}' (top, slot MID+1-j) / H_{MID+j-1}' (bottom,
+          // slot N-j): column rr, entries h6..h6+5 (LDS offsets are unsigned, so the bases
+          // sit at the lowest slot a chain reaches)
+          lds_cd* const Ob = GHr + (GS * (cr == 0 ? 1 : N - MID) + (cr == 0 ? 0 : kSlotPad<N>) + rr_ + RS * h6);
+          if (t < 64) {
+            // the sweeps are every wave's critical path (the other waves of the instance
+            // wait at the barrier): issue them ahead of a co-resident instance's phases
+            __builtin_amdgcn_s_setprio(3);
+            // right-hand side of step j (rows 0 / 1 add it): top stage j (slot j), bottom
+            // stage N-1-j (slot MID+1+j; the meeting stage MID at the bottom's step BOT,
+            // slot MID, which the bottom re-reads in the steps it does not take); na at +12N
+            lds_cd* const Bb = (lds_cd*)&sh.u.it.bo[0][0] + (12 * (cr == 0 ? 0 : MID + 1) + rr_);
+            lds_cd* const Bm = (lds_cd*)&sh.u.it.bo[MID][rr_];
+            auto rhs = [&](int j) __attribute__((always_inline)) -> lds_cd* {  // j: a constant
+              return (j >= BOT && cr != 0) ? Bm : Bb + 12 * j;
+            };
+            // the index a lane holds in the broadcast layout (rows 2 / 3: rotated by six)
+            const int ri = hi ? (rr_ < 6 ? rr_ + 6 : rr_ - 6) : rr_;
+            lds_d* const sink = (lds_d*)&sh.red[0] + (t & 31);
+            // y of step j's stage from rows 0 / 1 (top slot j, bottom slot MID+1+j: SIG)
+            lds_d* const Yh = (hi == 0 && s < 12) ? (lds_d*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? 0 : MID + 1) + rr_)
+                                                  : sink;
+            // y_kk(0) = b of the chain's first stage, in the broadcast layout; the next two
+            // right-hand sides in the output layout (published by the barrier just passed:
+            // loaded together, waited for once)
+            lds_cd* const B0 = (lds_cd*)&sh.u.it.bo[0][0] + (12 * (cr == 0 ? 0 : MID + 1) + ri);
+            double s0 = B0[0], s1 = B0[12 * N];
+            double c0 = rhs(1)[0], c1 = rhs(1)[12 * N];
+            asm volatile("" : "+v"(s0), "+v"(s1), "+v"(c0), "+v"(c1));
+            double src = s0 + s1;
+            *Yh = src;  // (rows 0 / 1: the broadcast layout is the output layout)
+            double bcn = hi ? 0.0 : c0 + c1;
+            double b0 = rhs(2)[0], b1 = rhs(2)[12 * N];
+#pragma unroll
+            for (int j = 1; j <= MID + 1; ++j) {
+              asm volatile("" : : : "memory");
+              double gc[6];
+#pragma unroll
+              for (int i = 0; i < 6; ++i) gc[i] = g[i];
+              const double bc = j <= MID ? bcn : 0.0;
+              if (j < MID) {  // prefetch the next step's rows
+                row6(rowp(j + 1));
+              } else if (j == MID) {  // the meeting step: M^{-1} (slot 0) and b_m in the broadcast layout
+                row6(GHr + RS * rr_ + h6);
+                lds_cd* qb = (lds_cd*)&sh.u.it.bo[MID][ri];
+                b0 = qb[0]; b1 = qb[12 * N];
+              } else {  // the last step: the first outward step's columns
+#pragma unroll
+                for (int i = 0; i < 6; ++i) g[i] = Ob[RS * i + GS * (MID - 1)];
+              }
+              asm volatile("" : : : "memory");  // the prefetch is issued here, not sunk to its use
+              double s_in = src;
+              if (j == MID + 1) s_in = row_pair_sum(src) - (b0 + b1);
+              const double y = pair_sum32(bdot6(gc, s_in, bc));
+              // the next right-hand side is summed after the chain: its loads were issued at
+              // the end of the previous step, and summing them ahead of the chain would put
+              // their LDS latency on the critical path
+              asm volatile("" : "+v"(b0), "+v"(b1));
+              if (j < MID) bcn = hi ? 0.0 : b0 + b1;
+              if (j + 2 <= MID) {
+                b0 = rhs(j + 2)[0]; b1 = rhs(j + 2)[12 * N];
+              }
+              const double yb = hi ? dppd<0x12A>(y) : y;  // row_ror:10: lane q <- lane q + 6
+              if (j <= MID) {
+                // y of stage kk(j) (the meeting stage's y_m / v_m stay in registers); the
+                // bottom chain keeps its v_m through the steps past BOT
+                if (j < MID) *((cr == 0 || j < BOT) ? Yh + 12 * j : sink) = y;
+                const bool adv = j <= BOT || cr == 0;
+                src = adv ? yb : src;
+              } else {
+                xp = yb;
+                if (cr == 0 && hi == 0 && s < 12) sh.u.it.xs[SIGX<N>(MID + 1)][rr_] = y;
+              }
+            }
+            STAMP(6);
+          }
+          {
+            // w_k = S_k^{-1} y_k for every stage but the meeting one, stage-parallel: lane
+            // LN(ph) of stage k's row takes row ph of S_k^{-1} and y_k by row broadcast
+            sync_all();
+            using scd2 = std::conditional_t<BIG, const dbl2, lds_cd2>;
+            const scd2* const q = (scd2*)(SmR + SLOT<N>(SIG<N>(k)) + RS * ph);
+            double srow[12];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+              const dbl2 v = q[i];
+              srow[2 * i] = v.x;
+              srow[2 * i + 1] = v.y;
+            }
+            // (the meeting stage has no y / w: its lanes read stage 0's y, their product unused)
+            double* const yk = &sh.u.it.yv[SIG<N>(k == MID ? 0 : k)][ph];
+            const double wk = bdot_ln12(srow, *yk, 0.0);
+            // in place: the row's reads of y_k precede (DPP operands); phantom rows keep out
+            // (stage N-1's row may sit in another wave and read y after their store)
+            if (cl && k != MID && !phantom) *yk = wk;
+            sync_all();
+          }
+          if (t < 64) {
+            // Outward step j: top kk = MID-j: X_kk = w_kk - G_{kk+1}' X_{kk+1}; bottom
+            // kk = MID+j: X_kk = w_kk - H_{kk-1}' X_{kk-1}.  w of stage kk: top slot MID-j,
+            // bottom slot N-j (Wb - 12 j); X_kk = xs[kk+1]: top slot MID+1-j, bottom slot
+            // N-j (SIGX; Xb - 12 j).  Even N: the bottom chain has no step MID (its store
+            // goes to the sink).  (bases at step MID's slot: step j at base + 12 (MID - j))
+            lds_cd* const Wb = (lds_cd*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? 0 : N - MID) + rr_);
+            lds_d* const sinkO = (lds_d*)&sh.red[0] + (t & 31);
+            lds_d* const Xb = (hi == 0 && s < 12) ? (lds_d*)&sh.u.it.xs[0][0] + (12 * (cr == 0 ? 1 : N - MID) + rr_)
+                                                  : sinkO;
+            double bq = Wb[12 * (MID - 1)];
+#pragma unroll
+            for (int j = 1; j <= MID; ++j) {
+              asm volatile("" : : : "memory");
+              double gc[6];
+#pragma unroll
+              for (int i = 0; i < 6; ++i) gc[i] = g[i];
+              const double bc = hi ? 0.0 : bq;
+              if (j < MID) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) g[i] = Ob[RS * i + GS * (MID - j - 1)];
+                // (even N: the bottom chain has no step MID; it re-reads its last w)
+                if (j + 1 <= BOT) bq = Wb[12 * (MID - j - 1)];
+                else bq = Wb[12 * (MID - (cr == 0 ? j + 1 : BOT))];
+              }
+              asm volatile("" : : : "memory");
+              const double x = pair_sum32(bdot6(gc, xp, bc));  // x = w - G' x_next with -G stored
+              if (j < MID) {
+                xp = hi ? dppd<0x12A>(x) : x;
+                Xb[12 * (MID - j)] = x;
+              } else if constexpr (N & 1) {
+                *Xb = x;
+              } else {  // even N: the bottom chain has no step MID
+                *(cr == 0 ? Xb : sinkO) = x;
+              }
+            }
+            __builtin_amdgcn_s_setprio(0);
+          }
+          wave_sync();
+          }  // MPCQ_REP_SWEEP
+      };
+      auto ph_sweep_lag = [&]() __attribute__((always_inline)) {
+          // P5-P7: the state solve on wave 0 alone (no block barrier inside), up to 32
+          // stages (beyond: ph_sweep_split).
           // Inward step j = 1..MID: top kk(j) = j, bottom kk(j) = N-1-j.  Half 0 (rows
           // 0 top / 1 bottom) runs the recurrence y_kk = b_kk - G_kk y_kk(j-1) (G_kk of
           // the top in GH[kk], H_kk of the bottom in GH[kk+1], stored negated), one
@@ -1617,21 +1826,12 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // top slot j-2 / bottom slot MID-1+j.  Step 1's rows are iteration-invariant:
           // wave 0 reads them before the barrier that publishes the right-hand sides.
           // (N > 32: S^{-1} is global, so the row pointer is a generic one)
-          // WPH (beyond 32 stages, where S^{-1} lives in L2): the S^{-1} products leave the
-          // sweep -- half 0 stores each y_k, and between the inward and the outward sweep
-          // every stage row turns its own y_k into w_k = S_k^{-1} y_k (one L2 round trip
-          // for all stages, instead of one per inward step on the sweep wave); half 1
-          // then shadows half 0 (same LDS rows, results to the sink).
-          constexpr bool WPH = BIG;
-          const int hh = WPH ? 0 : half;  // the row walk a lane follows
           using swp = lds_cd;
           using swp2 = lds_cd2;
           swp* const GHs = GHr;
           // (the bottom chain's slots are past N/2: +2, SLOT)
-          swp* Mb;
-          if constexpr (WPH) Mb = GHs + (GS * (cr == 0 ? 0 : MID) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_);
-          else Mb = half == 0 ? GHs + (GS * (cr == 0 ? 0 : MID) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_)
-                              : (swp*)SmR + (GS * (cr == 0 ? -2 : MID - 1) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_);
+          swp* const Mb = half == 0 ? GHs + (GS * (cr == 0 ? 0 : MID) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_)
+                                    : (lds_cd*)&sh.Sm[0][0] + (GS * (cr == 0 ? -2 : MID - 1) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_);
           double g[12];
           auto row12 = [&](swp* q) __attribute__((always_inline)) {  // 16-B aligned row: 6 ds_read_b128
 #pragma unroll
@@ -1647,8 +1847,8 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // chain's own, and their products are discarded by the hand-off select / the sink
           auto rowp = [&](int j) __attribute__((always_inline)) -> swp* {
             if (j >= 2 && j <= BOT) return Mb + GS * j;
-            const int jj = hh == 0 ? (cr == 0 ? j : (j < BOT ? j : BOT))
-                                   : (cr == 0 ? (j > 2 ? j : 2) : (j < BOT + 1 ? j : BOT + 1));
+            const int jj = half == 0 ? (cr == 0 ? j : (j < BOT ? j : BOT))
+                                     : (cr == 0 ? (j > 2 ? j : 2) : (j < BOT + 1 ? j : BOT + 1));
             return Mb + GS * jj;
           };
           if (t < 64) row12(rowp(1));
@@ -1674,11 +1874,8 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             // w of stage kk(j-2) (half 1): top slot j-2, bottom slot MID-1+j; the other
             // lanes store into the sink with the same stride
             lds_d* const sink = (lds_d*)&sh.red[0] + (t & 31);
-            lds_d* const Yb = (!WPH && half == 1 && s < 12)
-                                  ? (lds_d*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? -2 : MID - 1) + rr_) : sink;
-            // WPH: y of step j's stage (top slot j, bottom slot MID+1+j: SIG) from half 0
-            lds_d* const Yh = (WPH && half == 0 && s < 12)
-                                  ? (lds_d*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? 0 : MID + 1) + rr_) : sink;
+            lds_d* const Yb = (half == 1 && s < 12) ? (lds_d*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? -2 : MID - 1) + rr_)
+                                                    : sink;
             // right-hand sides run two steps ahead: step j sums the one of step j+1
             // (loaded during step j-1) and loads the one of step j+2; half 1 (the w
             // products) starts its chain from 0.  The first two (y_kk(0) and step 1's)
@@ -1689,7 +1886,6 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             double c0 = rhs(1)[0], c1 = rhs(1)[12 * N];
             asm volatile("" : "+v"(s0), "+v"(s1), "+v"(c0), "+v"(c1));
             double src = half == 0 ? s0 + s1 : 0.0;  // y_kk(0) (half 0)
-            if constexpr (WPH) *Yh = src;
             double bcn = (c0 + c1) * m0;
             double b0 = rhs(2)[0], b1 = rhs(2)[12 * N];
 #pragma unroll
@@ -1702,7 +1898,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               if (j < MID) {  // prefetch the next step's rows
                 row12(rowp(j + 1));
               } else if (j == MID) {  // the meeting step: M^{-1} rows (half 0), the S walk (half 1)
-                row12(hh == 0 ? GHs + RS * rr_ : rowp(MID + 1));
+                row12(half == 0 ? GHs + RS * rr_ : rowp(MID + 1));
                 lds_cd* qb = (lds_cd*)&sh.u.it.bo[MID][rr_];
                 b0 = qb[0]; b1 = qb[12 * N];
               } else {  // the last step: the first outward step's columns
@@ -1721,9 +1917,6 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               if (j + 2 <= MID) {
                 b0 = rhs(j + 2)[0]; b1 = rhs(j + 2)[12 * N];
               }
-              if constexpr (WPH) {  // y of stage kk(j) (the meeting stage's y_MID / v_MID stay in registers)
-                if (j < MID) *((cr == 0 || j < BOT) ? Yh + 12 * j : sink) = acc;
-              }
               if (j >= 2 && j <= MID) {  // half 1: w of stage kk(j-2)
                 Yb[12 * j] = acc;
               } else if (j == MID + 1) {  // even N: the bottom's kk(MID-1) is the meeting stage (no w)
@@ -1741,27 +1934,6 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               }
             }
             STAMP(6);
-          }
-          if constexpr (WPH) {
-            // w_k = S_k^{-1} y_k for every stage but the meeting one, stage-parallel: lane
-            // LN(ph) of stage k's row takes row ph of S_k^{-1} (L2) and y_k by row broadcast,
-            // the same products in the same order as the lagging half's (bit-identical)
-            sync_all();
-            using wcd2 = const dbl2;
-            const dbl2* const q = (wcd2*)(SmR + SLOT<N>(SIG<N>(k)) + RS * ph);
-            double srow[12];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-              const dbl2 v = q[i];
-              srow[2 * i] = v.x;
-              srow[2 * i + 1] = v.y;
-            }
-            double* const yk = &sh.u.it.yv[SIG<N>(k)][ph];
-            const double wk = bdot_ln12(srow, *yk, 0.0);
-            // in place: the row's reads of y_k precede (DPP operands); phantom rows keep out
-            // (stage N-1's row may sit in another wave and read y after their store)
-            if (cl && k != MID && !phantom) *yk = wk;
-            sync_all();
           }
           if (t < 64) {
             // Outward step j: top kk = MID-j: X_kk = w_kk - G_{kk+1}' X_{kk+1}; bottom
@@ -1806,6 +1978,11 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           }
           wave_sync();
           }  // MPCQ_REP_SWEEP
+      };
+      // the state sweep: the lagging form up to 32 stages, the split form beyond
+      auto ph_sweep = [&]() __attribute__((always_inline)) {
+        if constexpr (BIG) ph_sweep_split();
+        else ph_sweep_lag();
       };
       auto ph_recover = [&](const RhsOps* op, double uf, double beta, double& sf, double& sX, double (&ax)[3])
           __attribute__((always_inline)) {

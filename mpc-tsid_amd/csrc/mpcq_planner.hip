@@ -230,6 +230,75 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
   }
 
   // ---- getRefStates (FootstepPlanner.py:76-159)
+  // (N + 1 <= 64: one column per lane, the round-2 code as measured; WIDE: the same
+  // arithmetic per column, lane j also owning column j + 64)
+  if constexpr (!WIDE) {
+  if (a.ops & MPCQ_PLAN_REFSTATES) {
+    const int j = lane;
+    const double Tg = pp.T_gait, dt = pp.dt;
+    if (col && j >= 1) {
+      const double yaw = linspace_at(0.0, Tg - dt, N, j - 1) * vr[5];
+      const double c = cos(yaw), s = sin(yaw);
+      x[6] = vr[0] * c - vr[1] * s;
+      x[7] = vr[0] * s + vr[1] * c;
+      sh.v6[j] = x[6];
+      sh.v7[j] = x[7];
+    }
+    __syncthreads();
+    if (col && j >= 1) {
+      double a0 = 0.0, a1 = 0.0;  // np.cumsum: left to right
+      for (int i = 1; i <= j; ++i) {
+        a0 += sh.v6[i];
+        a1 += sh.v7[i];
+      }
+      x[0] = dt * a0 + st[0];
+      x[1] = dt * a1 + st[1];
+      if (a.k == 0) x[2] = pp.h_ref;
+      x[5] = vr[5] * linspace_at(dt, Tg, N, j - 1);
+      x[11] = vr[5];
+    }
+    if (j == 0) {
+#pragma unroll
+      for (int r = 0; r < 12; ++r) x[r] = st[r];
+    }
+    // height / rotation command state machine (uniform per instance)
+    int flag = sh.flag;
+    double h_rot = sh.in[37];
+    const double step = pp.cmd_threshold;
+    const double v2 = vr[2];
+    if (fabs(v2) > step && flag != 1) flag = 1;
+    int branch = 0;
+    if (fabs(v2) > step && flag == 1) {
+      h_rot += v2 * dt;
+      branch = 1;
+    } else if (fabs(v2) < step && flag == 1) {
+      flag = 2;
+      branch = 2;
+    } else if (flag == 0) {
+      branch = 3;
+    }
+    if (col && j >= 1) {
+      if (branch == 1) { x[2] = h_rot; x[8] = v2; }
+      else if (branch == 2) { x[8] = 0.0; x[9] = 0.0; x[10] = 0.0; }
+      else if (branch == 3) { x[2] = pp.h_ref; x[8] = 0.0; }
+      if (flag != 0) {
+        const double to = linspace_at(0.0, Tg - dt, N, j - 1);
+        x[3] = st[3] + vr[3] * to;  // xref[3, 0] was just set to abg[0]
+        x[4] = st[4] + vr[4] * to;
+        x[9] = vr[3];
+        x[10] = vr[4];
+      }
+    }
+    if (col) {
+#pragma unroll
+      for (int r = 0; r < 12; ++r) gx[r * NP + j] = x[r];
+    }
+    if (lane == 0) {
+      a.rot_flag[b] = flag;
+      a.h_rot[b] = h_rot;
+    }
+  }
+  } else {
   if (a.ops & MPCQ_PLAN_REFSTATES) {
     const double Tg = pp.T_gait, dt = pp.dt;
     // a second column per lane only when N + 1 > 64 (N = 64: column 64 on lane 0)
@@ -311,6 +380,7 @@ __global__ __launch_bounds__(64) void planner_kernel(mpcq_planner_params pp, Pla
       a.rot_flag[b] = flag;
       a.h_rot[b] = h_rot;
     }
+  }
   }
   if (lane == 0 && a.status) a.status[b] = 0;
 }

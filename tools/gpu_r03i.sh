@@ -1,0 +1,7 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/r03i_pytest_gpu.log 2>&1 &&
+timeout -k 10 300 python -u tools/iterbench.py --N 16 --reps 3 > $O/r03i_iter16.txt 2>&1 &&
+timeout -k 10 300 python -u tools/iterbench.py --N 48 --reps 2 > $O/r03i_iter48.txt 2>&1 &&
+timeout -k 10 300 python -u bench.py > $O/r03i_bench_c2.json 2> $O/r03i_bench_c2.err

@@ -1089,22 +1089,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     double pri_res = 0.0, dua_res = 0.0, eps_pri = 0.0, eps_dua = 0.0, s_pri = 0.0, s_dua = 0.0;
   // per-lane constants of the ADMM loop and the residuals: LDS offsets, flags
     const bool hp = k >= 1, isv = ph >= 6;
-    const int oXd = xo;                                                // Xd(k, ph)
-    const int oHd = XO<N>(hp ? k - 1 : 0, ph) + (ph < 6 ? 1 : 2);      // Hd(k, ph)
-    const int oH6 = XO<N>(hp ? k - 1 : 0, ph < 6 ? ph + 6 : 11) + 1;   // H6(k, ph)
-    const int oF = fo;
-    const int ta = cl ? c : 3;  // first own friction row
-    const bool ta0 = (ta >> 1) == 0;
-    const int oFa = FO<N>(k, f, ta >> 1) + 5 + (ta & 1), oFb = FO<N>(k, f, 2) + 5 + ta;
-    const int oF4 = FO<N>(k, f, 2) + 9;
-    const int oFW = 72 * k + 6 * ph, oFWc = 72 * k + (isv ? ph - 6 : 0);
-    const int oQL = 36 * k + 6 * (isv ? ph - 6 : 0);
-    const int oXSp = 12 * k + ph, oXSp6 = 12 * k + (ph < 6 ? ph + 6 : ph);  // natural order (update_info)
-    // the sweep's states in its slots (SIGX): own X_{k+1}, the previous stage's X_k
-    const int rXS = 12 * SIGX<N>(k + 1) + ph, rXSp = 12 * SIGX<N>(k) + ph,
-              rXSp6 = 12 * SIGX<N>(k) + (ph < 6 ? ph + 6 : ph);
     const int zXS = (int)(sh.zero - &sh.u.it.xs[0][0]);  // X_0 is not stored: stage 0 reads zeros
-    const int rXSpm = hp ? rXSp : zXS, rXSp6m = hp ? rXSp6 : zXS;
     const double m2 = cc == 2 ? 1.0 : 0.0;
     // masked variants for the loop: a lane whose term is structurally absent reads a
     // zero (stage 0 has no previous stage; H6 only on the position rows; the force Schur
@@ -1112,15 +1097,66 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     int zAb;  // offset of a zero block from Ab (masked reads)
     if constexpr (ABG) zAb = Work<N>::ZERO - Work<N>::AB;
     else zAb = (int)(sh.zero - sh.Ab);
-    const int oHdm = hp ? oHd : zAb;
-    const int oH6m = hp && !isv ? oH6 : zAb;
-    const int oFWcm = isv ? oFWc : zFW;
-    const int oQLm = isv ? oQL : zQL;
     lds_cd* XSr = (lds_cd*)&sh.u.it.xs[0][0];
-    double* const Wbo = &sh.u.it.bo[SIG<N>(k)][ph];
-    double* const Wna = &sh.u.it.na[SIG<N>(hp ? k - 1 : N - 1)][ph];
     double* const Wdump = &sh.dump[t & 63];
-    const int oB0 = FO<N>(k, 0, 0) + (ph >= 9 ? ph - 8 : 0);  // B row ph on force (fp, cp): + 24 fp + 7 cp
+    // The LDS offsets of the lane's coefficients, derived from its coordinates.  O0
+    // is derived once and held (the loop phases up to 32 stages, where the ADMM loop
+    // has the registers); a phase run between long stretches of other work -- the
+    // termination check at every N, every loop phase beyond 32 stages (168 VGPRs) --
+    // re-derives them from freshly laundered coordinates (MPCQ_LANE_OFFS(true)), a
+    // few integer ops each: held across the ADMM loop, the compiler spills them, and
+    // each use then waits on its own scratch round trip (the reloads sit right in
+    // front of their LDS reads, one after another).
+    struct LaneOffs {
+      int oXd, oHd, oH6, oF, oFa, oFb, oF4, oFW, oQL, oXSp, oXSp6, rXS, rXSpm, rXSp6m, oHdm, oH6m, oFWcm, oQLm,
+          oB0;
+      bool ta0;
+      double* Wbo;
+      double* Wna;
+    };
+    auto offs = [&]() __attribute__((always_inline)) -> LaneOffs {
+      const bool hp_ = k >= 1, isv_ = ph >= 6;
+      LaneOffs o;
+      o.oXd = xo;                                                 // Xd(k, ph)
+      o.oHd = XO<N>(hp_ ? k - 1 : 0, ph) + (ph < 6 ? 1 : 2);      // Hd(k, ph)
+      o.oH6 = XO<N>(hp_ ? k - 1 : 0, ph < 6 ? ph + 6 : 11) + 1;   // H6(k, ph)
+      o.oF = fo;
+      const int ta = c < 3 ? c : 3;  // first own friction row
+      o.ta0 = (ta >> 1) == 0;
+      o.oFa = FO<N>(k, f, ta >> 1) + 5 + (ta & 1);
+      o.oFb = FO<N>(k, f, 2) + 5 + ta;
+      o.oF4 = FO<N>(k, f, 2) + 9;
+      o.oFW = 72 * k + 6 * ph;
+      const int oFWc = 72 * k + (isv_ ? ph - 6 : 0);
+      o.oQL = 36 * k + 6 * (isv_ ? ph - 6 : 0);
+      o.oXSp = 12 * k + ph;  // natural order (update_info)
+      o.oXSp6 = 12 * k + (ph < 6 ? ph + 6 : ph);
+      // the sweep's states in its slots (SIGX): own X_{k+1}, the previous stage's X_k
+      o.rXS = 12 * SIGX<N>(k + 1) + ph;
+      o.rXSpm = hp_ ? 12 * SIGX<N>(k) + ph : zXS;
+      o.rXSp6m = hp_ ? 12 * SIGX<N>(k) + (ph < 6 ? ph + 6 : ph) : zXS;
+      o.oHdm = hp_ ? o.oHd : zAb;
+      o.oH6m = hp_ && !isv_ ? o.oH6 : zAb;
+      o.oFWcm = isv_ ? oFWc : zFW;
+      o.oQLm = isv_ ? o.oQL : zQL;
+      o.oB0 = FO<N>(k, 0, 0) + (ph >= 9 ? ph - 8 : 0);  // B row ph on force (fp, cp): + 24 fp + 7 cp
+      o.Wbo = &sh.u.it.bo[SIG<N>(k)][ph];
+      o.Wna = &sh.u.it.na[SIG<N>(hp_ ? k - 1 : N - 1)][ph];
+      return o;
+    };
+    const LaneOffs O0 = offs();
+#define MPCQ_LANE_OFFS(RECOMP)                                                                              \
+  if constexpr (RECOMP) launder();                                                                         \
+  const LaneOffs O_ = (RECOMP) ? offs() : O0;                                                              \
+  [[maybe_unused]] const int oXd = O_.oXd, oHd = O_.oHd, oH6 = O_.oH6, oF = O_.oF, oFa = O_.oFa,           \
+                             oFb = O_.oFb, oF4 = O_.oF4, oFW = O_.oFW, oQL = O_.oQL, oXSp = O_.oXSp,       \
+                             oXSp6 = O_.oXSp6, rXS = O_.rXS, rXSpm = O_.rXSpm, rXSp6m = O_.rXSp6m,         \
+                             oHdm = O_.oHdm, oH6m = O_.oH6m, oFWcm = O_.oFWcm, oQLm = O_.oQLm, oB0 = O_.oB0; \
+  [[maybe_unused]] const bool ta0 = O_.ta0;                                                                \
+  [[maybe_unused]] double* const Wbo = O_.Wbo;                                                             \
+  [[maybe_unused]] double* const Wna = O_.Wna
+    // beyond 32 stages the loop phases re-derive them too
+    constexpr bool kRecompLoop = BIG;
     auto launder_p = [&]() __attribute__((always_inline)) {
       lds_uniform(Ab); lds_uniform(GHr); lds_uniform(SmR); lds_uniform(FWr); lds_uniform(QLr); lds_uniform(XSr);
     };
@@ -1144,7 +1180,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     auto colF_off = [&](const double (&v)[3]) __attribute__((always_inline)) -> double {
       double A[10];
 #pragma unroll
-      for (int i = 0; i < 10; ++i) A[i] = Ab[oF + i];
+      for (int i = 0; i < 10; ++i) A[i] = Ab[fo + i];
       return colF_c(A, v);
     };
     // max over a 16-lane row: quad xor 1, xor 2, then rotations by 4 and 8
@@ -1157,6 +1193,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     };
     // A v on the own rows for own-column values (vf, vX), the previous stage's states in P
     auto rowA = [&](double vf, double vX, lds_cd* P, double (&ax)[3]) __attribute__((always_inline)) {
+      MPCQ_LANE_OFFS(true);
       double bco[12];
 #pragma unroll
       for (int psi = 0; psi < 12; ++psi) {
@@ -1182,6 +1219,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     // A' w on the own columns for own-row values w, the next stage's dynamics-row w in W
     auto colAt = [&](const double (&w)[3], const double* W, double& atf, double& atX)
         __attribute__((always_inline)) {
+      MPCQ_LANE_OFFS(true);
       atf = colF_off(w);
       const double* wn = W + 12 * (k < N - 1 ? k + 1 : k);
       const double sXv = Ab[oXd] * w[0];
@@ -1570,6 +1608,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         double cf[10], fwc[12], cXd, cHd, cH6;
       };
       auto load_rhs_ops = [&](RhsOps& o) __attribute__((always_inline)) {
+        MPCQ_LANE_OFFS(kRecompLoop);
 #pragma unroll
         for (int i = 0; i < 10; ++i) o.cf[i] = Ab[oF + i];
 #pragma unroll
@@ -1586,6 +1625,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           RhsOps own_;
           if (!op) load_rhs_ops(own_);
           const RhsOps& o = op ? *op : own_;
+          MPCQ_LANE_OFFS(kRecompLoop);
           // P1-P4: w = rho z - y; b_f = sigma x_f + A_f' w and u = F b_f, beta = R B u
           // (stage-local, DPP only); then the sweep right-hand side of the own state
           // column (bo) and this stage's dynamics-row terms of stage k-1's state
@@ -1989,6 +2029,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // P8: forces f_k = F_k (b_f - R B' g) = u - (F W) g, with g = Xd X_{k+1} + Hd X_k
           // on the velocity rows (the states' part of those rows)
           double gv;
+          MPCQ_LANE_OFFS(kRecompLoop);
           // the iteration-invariant LDS operands of P8 / P9 are read before the
           // barrier that ends the sweeps (their latency hides behind it), the
           // sweep's states after it

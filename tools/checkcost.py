@@ -1,6 +1,6 @@
 """Cost of one termination check / rho-adaptation step, measured on the production kernel.
 
-    python tools/checkcost.py
+    python tools/checkcost.py [--N 16]
 
 Runs 256 copies of one C2 instance (one per CU) with adaptive rho off and
 max_iter fixed, so every configuration runs exactly max_iter iterations, and
@@ -18,11 +18,16 @@ sys.path.insert(0, os.path.join(REPO, "mpc-tsid_amd"))
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--N", type=int, default=16)
+    ap.add_argument("--iters", type=int, default=2000)
+    a = ap.parse_args()
     import torch
     import mpcq
     dev = torch.device("cuda", 0)
-    src = mpcq.synth.make_batch(1024, 16, gaits=("trot",), seed=2)
-    B, iters = 256, 2000
+    src = mpcq.synth.make_batch(1024, a.N, gaits=("trot",), seed=2)
+    B, iters = 256, a.iters
     xr = torch.from_numpy(np.ascontiguousarray(np.repeat(src["xref"][:1], B, axis=0))).to(dev)
     fs = torch.from_numpy(np.ascontiguousarray(np.repeat(src["fsteps"][:1], B, axis=0))).to(dev)
     f0 = torch.empty((B, 12), dtype=torch.float64, device=dev)
@@ -30,7 +35,7 @@ def main():
     it = torch.empty(B, dtype=torch.int32, device=dev)
     base = None
     for chk in (0, 100, 25, 5):
-        eng = mpcq.Engine(16, adaptive_rho=0, max_iter=iters, check_termination=chk, eps_abs=1e-30, eps_rel=1e-30)
+        eng = mpcq.Engine(a.N, adaptive_rho=0, max_iter=iters, check_termination=chk, eps_abs=1e-30, eps_rel=1e-30)
         ms = []
         for _ in range(5):
             eng.solve_device(B, xr.data_ptr(), fs.data_ptr(), f0.data_ptr(), st.data_ptr(), it.data_ptr())

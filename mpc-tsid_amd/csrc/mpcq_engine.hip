@@ -1244,8 +1244,54 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     // at the check's tolerances, 4 / 8 at the approximate (x10) ones
     int inf_bits = 0;
     int inf_need = 0;  // cheap-condition bits (same layout) awaiting the products
+    // The termination check's scaling constants (fixed once the Ruiz scaling is done):
+    // D, D^-1 of the own columns, E^-1 of the own rows, the scaled P diagonal, c and
+    // 1/c.  Held across the ADMM loop, which does not use them, they were spilled and
+    // each use in the check waited on its own scratch reload; they are stored once in
+    // private memory instead and read back in a batch at the top of each check phase
+    // (through a laundered pointer: never forwarded from the store, so nothing derived
+    // from them is hoisted out of the loop either; cached scratch loads, not volatile
+    // ones, which would bypass the caches).  Values and rounding are the ones the check
+    // computed before (1.0 / Df etc.).
+    enum { CK_DF, CK_DX, CK_DFI, CK_DXI, CK_EI0, CK_EI1, CK_EI2, CK_PBF, CK_PBX, CK_C, CK_CI, CK_COUNT };
+    using pdbl = __attribute__((address_space(5))) double;
+    double ck_mem_[CK_COUNT];
+    auto ck_ptr = [&]() __attribute__((always_inline)) -> pdbl* {
+      pdbl* q = (pdbl*)&ck_mem_[0];
+      asm volatile("" : "+v"(q));
+      return q;
+    };
+    // (beyond 32 stages the loop itself is short of registers: there the values are
+    // derived where used, as before -- held in memory they cost the loop a spill,
+    // N = 48 9.7 -> 10.4 us per iteration, profiles/r03k_iterbench.txt)
+    auto ck = [&](int i) __attribute__((always_inline)) -> double {
+      if constexpr (BIG) {
+        switch (i) {
+          case CK_DF: return Df;
+          case CK_DX: return DX;
+          case CK_DFI: return 1.0 / Df;
+          case CK_DXI: return 1.0 / DX;
+          case CK_EI0: return 1.0 / E[0];
+          case CK_EI1: return 1.0 / E[1];
+          case CK_EI2: return 1.0 / E[2];
+          case CK_PBF: return Pbf();
+          case CK_PBX: return PbX();
+          case CK_C: return cscale;
+          default: return 1.0 / cscale;
+        }
+      } else {
+        return ck_ptr()[i];
+      }
+    };
+    // The check's lane ids, re-derived from a laundered thread index: the red[] addresses
+    // built from them would otherwise be hoisted out of the ADMM loop and spilled too.
+#define MPCQ_CHECK_IDS()                                           \
+  int tl_ = t;                                                     \
+  asm volatile("" : "+v"(tl_));                                    \
+  [[maybe_unused]] const int wv = tl_ >> 6, lane = tl_ & 63, s = tl_ & 15
     double dyp[3];     // delta_y projected onto the polar of the recession cone of [l, u]
     auto infeas_cheap = [&](const double (&dy)[3], double dxf, double dxX) __attribute__((always_inline)) {
+      MPCQ_CHECK_IDS();
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const bool uinf = hi_of(j) > kInf * kMinScaling, linf = lo_of(j) < -kInf * kMinScaling;
@@ -1267,10 +1313,13 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       }
       if (phantom) ineq = 0.0;  // a sum: stage N-1 counts once
       double q3[2] = {0.0, 0.0};
-      if (cl) {
-        const double dif = 1.0 / Df, diX = 1.0 / DX;
-        q3[0] = fmax(fabs(Df * dxf), fabs(DX * dxX));                    // ||D dx||
-        q3[1] = fmax(fabs(Pbf() * dxf * dif), fabs(PbX() * dxX * diX));  // ||D^-1 P dx||
+      {
+        const double df = ck(CK_DF), dx = ck(CK_DX), dif = ck(CK_DFI), diX = ck(CK_DXI);
+        const double pbf = ck(CK_PBF), pbx = ck(CK_PBX);
+        if (cl) {
+          q3[0] = fmax(fabs(df * dxf), fabs(dx * dxX));                // ||D dx||
+          q3[1] = fmax(fabs(pbf * dxf * dif), fabs(pbx * dxX * diX));  // ||D^-1 P dx||
+        }
       }
       // maxima over the wave (lanes 0, 2, 3 keep quantity s), the sum by xor butterflies
       double mx[3] = {ndy, q3[0], q3[1]}, mine = 0.0;
@@ -1299,6 +1348,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     // the products, where a cheap condition holds (inf_need != 0, uniform): A' dy for
     // the primal test, A dx for the dual one, on the deltas infeas_cheap published
     auto infeas_products = [&](double dxf, double dxX) __attribute__((always_inline)) {
+      MPCQ_CHECK_IDS();
       launder_p();
       double vu = -INFINITY, vl = -INFINITY;
       {
@@ -1315,7 +1365,8 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       {
         double dtf, dtX;
         colAt(dyp, &sh.u.it.nb[0][0], dtf, dtX);
-        if (cl) naty = fmax(fabs(dtf * (1.0 / Df)), fabs(dtX * (1.0 / DX)));  // ||D^-1 A' dy||
+        const double dif = ck(CK_DFI), diX = ck(CK_DXI);
+        if (cl) naty = fmax(fabs(dtf * dif), fabs(dtX * diX));  // ||D^-1 A' dy||
       }
       double mx[3] = {naty, vu, vl}, mine = 0.0;
 #pragma unroll
@@ -1352,12 +1403,16 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     // INF: after infeas_cheap, which has published the states / duals with its deltas
     auto update_info = [&](auto inf_tag) __attribute__((always_inline)) {
       constexpr bool INF = decltype(inf_tag)::value;
+      MPCQ_CHECK_IDS();
       if constexpr (!INF) {
         if (cl) { sh.u.it.yv[k][ph] = xX; sh.u.it.bo[k][ph] = y[0]; }
         sync_all();
       }
       STAMP(4);
       launder_p();
+      const double ei3[3] = {ck(CK_EI0), ck(CK_EI1), ck(CK_EI2)};
+      const double dif = ck(CK_DFI), diX = ck(CK_DXI), pbf = ck(CK_PBF), pbx = ck(CK_PBX);
+      const double cinv = ck(CK_CI), csc = ck(CK_C);
       lds_cd* const YV = (lds_cd*)&sh.u.it.yv[0][0];  // X_{k'} of stage k' >= 1 at 12 (k' - 1)
       double mine = 0.0;                              // this lane's row maximum (quantity s)
       {  // primal side: A x - z on the own rows
@@ -1365,7 +1420,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         rowA(xf, xX, YV, ax);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          const double ei = 1.0 / E[j], d = ax[j] - z[j];
+          const double ei = ei3[j], d = ax[j] - z[j];
           q6[0] = fmax(q6[0], fabs(ei * d));
           q6[1] = fmax(q6[1], fabs(ei * ax[j]));
           q6[2] = fmax(q6[2], fabs(ei * z[j]));
@@ -1384,8 +1439,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         double q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         double atf, atX;
         colAt(y, &sh.u.it.bo[0][0], atf, atX);
-        const double pxf = Pbf() * xf, pxX = PbX() * xX;
-        const double dif = 1.0 / Df, diX = 1.0 / DX;
+        const double pxf = pbf * xf, pxX = pbx * xX;
         const double df_ = pxf + atf, dX_ = pxX + atX;
         if (cl) {
           q6[0] = fmax(fabs(dif * df_), fabs(diX * dX_));
@@ -1413,7 +1467,6 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         for (int w = 1; w < NW; ++w) v = fmax(v, sh.red[32 * w + e]);
         gather_direct12(v, qv);
       }
-      const double cinv = 1.0 / cscale;
       pri_res = qv[0];
       dua_res = cinv * qv[6];
       eps_pri = p.eps_abs + p.eps_rel * fmax(qv[1], qv[2]);
@@ -1442,8 +1495,8 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         for (int fi = 0; fi < 2; ++fi) {
           const double f = fi == 0 ? 1.0 : 10.0, epi = f * p.eps_prim_inf, edi = f * p.eps_dual_inf;
           const bool pi = !(pri_res < f * eps_pri) && ndy > kDivTol && ineq < epi * ndy;
-          const bool di = !(dua_res < f * eps_dua) && ndx > kDivTol && 0.0 < cscale * edi * ndx &&
-                          npdx < cscale * edi * ndx;
+          const bool di = !(dua_res < f * eps_dua) && ndx > kDivTol && 0.0 < csc * edi * ndx &&
+                          npdx < csc * edi * ndx;
           need |= (pi ? 1 : 0) << (2 * fi);
           need |= (di ? 2 : 0) << (2 * fi);
         }
@@ -1574,6 +1627,12 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         cls |= cj << (2 * j);
       }
       set_rho();
+      if constexpr (!BIG) {
+        pdbl* const q = ck_ptr();
+        q[CK_DF] = Df; q[CK_DX] = DX; q[CK_DFI] = 1.0 / Df; q[CK_DXI] = 1.0 / DX;
+        q[CK_EI0] = 1.0 / E[0]; q[CK_EI1] = 1.0 / E[1]; q[CK_EI2] = 1.0 / E[2];
+        q[CK_PBF] = Pbf(); q[CK_PBX] = PbX(); q[CK_C] = cscale; q[CK_CI] = 1.0 / cscale;
+      }
       // warm start (osqp_warm_start: x = D^-1 x0, z = A x; y = c E^-1 y0)
       if (a.warm_x) {
         xf = a.warm_x[b * n + colF] / Df;
@@ -1608,7 +1667,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         double cf[10], fwc[12], cXd, cHd, cH6;
       };
       auto load_rhs_ops = [&](RhsOps& o) __attribute__((always_inline)) {
-        MPCQ_LANE_OFFS(kRecompLoop);
+        MPCQ_LANE_OFFS(true);  // (once per stretch of iterations)
 #pragma unroll
         for (int i = 0; i < 10; ++i) o.cf[i] = Ab[oF + i];
 #pragma unroll
@@ -2024,7 +2083,9 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         if constexpr (BIG) ph_sweep_split();
         else ph_sweep_lag();
       };
-      auto ph_recover = [&](const RhsOps* op, double uf, double beta, double& sf, double& sX, double (&ax)[3])
+      // ri0: 1/rho of the own slot-0 row (the ADMM loop's, or polish's)
+      auto ph_recover = [&](const RhsOps* op, double ri0, double uf, double beta, double& sf, double& sX,
+                            double (&ax)[3])
           __attribute__((always_inline)) {
           // P8: forces f_k = F_k (b_f - R B' g) = u - (F W) g, with g = Xd X_{k+1} + Hd X_k
           // on the velocity rows (the states' part of those rows)
@@ -2059,7 +2120,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           {
             {
               // B f on the velocity rows (zero coefficients elsewhere)
-              const double bfv = beta * ri[0] - bdot_ln6v(qll, gv, 0.0);
+              const double bfv = beta * ri0 - bdot_ln6v(qll, gv, 0.0);
               const double dyn = (gv + eH6 * xb) + bfv;
               // friction rows: lane c < 3 owns row c, lane 3 rows 3 and 4 (all loads unconditional)
               const double q0 = qbc<0>(sf), q1 = qbc<1>(sf), q2 = qbc<2>(sf);
@@ -2113,7 +2174,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // per lane, 17.68 -> 16.75 us per iteration, profiles/r03c_iterbench.txt)
           ph_rhs(true, kBig<N> ? nullptr : &ops, kNoW, 0.0, 0.0, uf, beta);
           ph_sweep();
-          ph_recover(kBig<N> ? nullptr : &ops, uf, beta, sf, sX, ax);
+          ph_recover(kBig<N> ? nullptr : &ops, ri[0], uf, beta, sf, sX, ax);
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
             const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
@@ -2284,7 +2345,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               }
               ph_rhs(false, nullptr, pw, p.sigma * xf, p.sigma * xX, uf, beta);
               ph_sweep();
-              ph_recover(nullptr, uf, beta, xpf, xpX, ax);
+              ph_recover(nullptr, ri[0], uf, beta, xpf, xpX, ax);
 #pragma unroll
               for (int j = 0; j < 3; ++j) {
                 axp[j] = ax[j];
@@ -2300,7 +2361,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               }
               ph_rhs(false, nullptr, pw, -Pbf() * xpf, -PbX() * xpX, uf, beta);
               ph_sweep();
-              ph_recover(nullptr, uf, beta, dxf, dxX, ax);
+              ph_recover(nullptr, ri[0], uf, beta, dxf, dxX, ax);
               xpf += dxf;
               xpX += dxX;
 #pragma unroll

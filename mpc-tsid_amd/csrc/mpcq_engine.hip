@@ -464,11 +464,28 @@ constexpr bool kBig = N > 32;
 // through the same accessors, the stage-parallel phases from L2.
 template <int N>
 constexpr bool kAbG = N > 49;
+// Beyond 48 stages (13-16 waves: 128 VGPRs) the F_k row is read from the workspace in
+// the loop and the z update's constants are batch-loaded from private memory instead
+// of being held; from 33 to 48 stages (168 VGPRs) holding them is faster.  Measured at
+// every horizon 33..64 with both, either and neither (tools/bigsweep.py,
+// profiles/r03o_bigsweep.txt: N = 48 9.05 us per iteration held vs 10.37 not; N = 56
+// 19.27 not held vs 20.06).  -DMPCQ_FR_HELD / -DMPCQ_ZC_HELD: held everywhere (experiments).
+#ifdef MPCQ_FR_HELD
+template <int N> constexpr bool kFrWork = false;
+#else
+template <int N> constexpr bool kFrWork = N > 48;
+#endif
+#ifdef MPCQ_ZC_HELD
+template <int N> constexpr bool kZcMem = false;
+#else
+template <int N> constexpr bool kZcMem = N > 48;
+#endif
 template <int N>
 struct Work {  // offsets (doubles) inside one instance's workspace
   // SM starts two slots in (a pad kept from round 2; the sweep no longer reads it)
+  // FR: each lane's row of F_k (12 doubles, lane-interleaved: entry i of thread t at 16 kRows i + t)
   static constexpr int SM = 2 * GS, FW = SM + N * GS + 2, QL = FW + 72 * N, ZERO = QL + 36 * N, AB = ZERO + 72,
-                       SIZE = AB + (kAbG<N> ? ((126 * N - 18 + 1) & ~1) : 0);
+                       FR = AB + (kAbG<N> ? ((126 * N - 18 + 1) & ~1) : 0), SIZE = FR + (N > 48 ? 12 * 16 * kRows<N> : 0);
 };
 
 template <int N>
@@ -553,6 +570,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
   using wcd = std::conditional_t<BIG, const double, lds_cd>;
   using wdd = std::conditional_t<BIG, double, lds_d>;
   wcd* SmR;
+  double* FRg = nullptr;  // (N > 32) this lane's F_k row in the workspace, stride 16 kRows
   lds_cd* FWr;
   wcd* QLr;
   wdd* SmW;
@@ -564,6 +582,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     SmW = wk + Work<N>::SM;
     FWW = (lds_d*)&sh.FWs[0][0];  // (Work<N>::FW stays reserved, unused)
     QLW = wk + Work<N>::QL;
+    FRg = wk + Work<N>::FR + t;
     zFW = (int)(sh.zero - &sh.FWs[0][0]);
     zQL = Work<N>::ZERO - Work<N>::QL;
     if (SOLVE && t < 72) wk[Work<N>::ZERO + t] = 0.0;
@@ -829,6 +848,32 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       }
     };
 
+    // Beyond 48 stages (kZcMem: 128 VGPRs) the ADMM loop spills, and the z / y update's
+    // per-row constants (bounds, rho, 1/rho) came back as one scratch reload per use,
+    // each waited for before the next.  There they are kept in private memory explicitly
+    // and read in one batch per use site (zc_ptr: a laundered pointer, so the loads are
+    // neither forwarded nor hoisted).
+    using pdbl = __attribute__((address_space(5))) double;
+    enum { ZC_LO = 0, ZC_HI = 3, ZC_RR = 6, ZC_RI = 9, ZC_COUNT = 12 };
+    double zc_mem_[kZcMem<N> ? ZC_COUNT : 1];
+    auto zc_ptr = [&]() __attribute__((always_inline)) -> pdbl* {
+      pdbl* q = (pdbl*)&zc_mem_[0];
+      asm volatile("" : "+v"(q));
+      return q;
+    };
+    auto zc_store = [&]() __attribute__((always_inline)) {
+      if constexpr (kZcMem<N>) {
+        pdbl* const q = zc_ptr();
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          q[ZC_LO + j] = lo_of(j);
+          q[ZC_HI + j] = hi_of(j);
+          q[ZC_RR + j] = rr[j];
+          q[ZC_RI + j] = ri[j];
+        }
+      }
+    };
+
     // ---- row / column operators --------------------------------------------
     // A v for own rows from own forces vf (column lanes), own states vX and the
     // previous stage's states in xs[k]; also returns the force gather.
@@ -966,6 +1011,10 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           Fr[psi] = v;
         }
         gj12(Fr, ph, ok);
+        if constexpr (kFrWork<N>) {
+#pragma unroll
+          for (int i = 0; i < 12; ++i) FRg[16 * NR * i] = Fr[i];
+        }
         // F W (row ph): W[psi][j] = rho_{6+j} B[6+j][psi]
         double fw[6];
 #pragma unroll
@@ -1254,7 +1303,6 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     // ones, which would bypass the caches).  Values and rounding are the ones the check
     // computed before (1.0 / Df etc.).
     enum { CK_DF, CK_DX, CK_DFI, CK_DXI, CK_EI0, CK_EI1, CK_EI2, CK_PBF, CK_PBX, CK_C, CK_CI, CK_COUNT };
-    using pdbl = __attribute__((address_space(5))) double;
     double ck_mem_[CK_COUNT];
     auto ck_ptr = [&]() __attribute__((always_inline)) -> pdbl* {
       pdbl* q = (pdbl*)&ck_mem_[0];
@@ -1627,6 +1675,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         cls |= cj << (2 * j);
       }
       set_rho();
+      zc_store();
       if constexpr (!BIG) {
         pdbl* const q = ck_ptr();
         q[CK_DF] = Df; q[CK_DX] = DX; q[CK_DFI] = 1.0 / Df; q[CK_DXI] = 1.0 / DX;
@@ -1685,6 +1734,16 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           if (!op) load_rhs_ops(own_);
           const RhsOps& o = op ? *op : own_;
           MPCQ_LANE_OFFS(kRecompLoop);
+          // beyond 48 stages (kFrWork) the F_k row is read from the workspace here (issued first,
+          // its latency behind the phase's other loads) instead of being held through
+          // the ADMM loop in 24 of the 128 VGPRs
+          double frg[12];
+          if constexpr (kFrWork<N>) {
+            const double* q = FRg;
+            asm volatile("" : "+v"(q));
+#pragma unroll
+            for (int i = 0; i < 12; ++i) frg[i] = q[16 * NR * i];
+          }
           // P1-P4: w = rho z - y; b_f = sigma x_f + A_f' w and u = F b_f, beta = R B u
           // (stage-local, DPP only); then the sweep right-hand side of the own state
           // column (bo) and this stage's dynamics-row terms of stage k-1's state
@@ -1695,11 +1754,24 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           double w[3];
 #pragma unroll
           for (int j = 0; j < 3; ++j) w[j] = admm ? rr[j] * z[j] - y[j] : pw[j];
+          if constexpr (kZcMem<N>) {
+            if (admm) {
+              pdbl* const q = zc_ptr();
+              const double r0 = q[ZC_RR], r1 = q[ZC_RR + 1], r2 = q[ZC_RR + 2];
+              w[0] = r0 * z[0] - y[0];
+              w[1] = r1 * z[1] - y[1];
+              w[2] = r2 * z[2] - y[2];
+            }
+          }
           // the phase's arithmetic starts after this point, the loads before it
           asm volatile("" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]) : : "memory");
           const double bf = colF_c(o.cf, w) + (admm ? p.sigma * xf : xcf);  // b_f = sigma x_f + A_f' w (- q, q = 0)
           // u = F b_f (kept for the forces) and beta = R B u = (F W)' b_f (rows 6..11)
-          uf = bdot_ln12(Fr, bf, 0.0);
+          if constexpr (kFrWork<N>) {
+            uf = bdot_ln12(frg, bf, 0.0);
+          } else {
+            uf = bdot_ln12(Fr, bf, 0.0);
+          }
           beta = bdot_ln12(o.fwc, bf, 0.0);
           {
             const double wd = w[0] - beta;  // dynamics-row w less the force Schur term (beta = 0 on rows 0..5)
@@ -1734,7 +1806,9 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // N = 32: 3.31 vs 3.92, profiles/r03h_iterbench.txt): the split saves six FMAs and
           // three row reads per step but adds the swap-add, the rotation and the selects,
           // and the stage-parallel S^{-1} phase with its two barriers.
-          const int hi = (t >> 5) & 1;  // rows 2 / 3: the second six terms
+          int tl_ = t;  // (laundered: the lane ids derived here are not hoisted out of the loop and spilled)
+          asm volatile("" : "+v"(tl_));
+          const int hi = (tl_ >> 5) & 1;  // rows 2 / 3: the second six terms
           const int h6 = 6 * hi;
 #ifndef MPCQ_REP_SWEEP
 #define MPCQ_REP_SWEEP 1
@@ -2174,13 +2248,25 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // per lane, 17.68 -> 16.75 us per iteration, profiles/r03c_iterbench.txt)
           ph_rhs(true, kBig<N> ? nullptr : &ops, kNoW, 0.0, 0.0, uf, beta);
           ph_sweep();
-          ph_recover(kBig<N> ? nullptr : &ops, ri[0], uf, beta, sf, sX, ax);
+          double zl[3], zh[3], zrr[3], zri[3];  // the update's per-row constants
+          if constexpr (kZcMem<N>) {
+            ph_recover(nullptr, zc_ptr()[ZC_RI], uf, beta, sf, sX, ax);
+            pdbl* const q = zc_ptr();
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              zl[j] = q[ZC_LO + j]; zh[j] = q[ZC_HI + j]; zrr[j] = q[ZC_RR + j]; zri[j] = q[ZC_RI + j];
+            }
+          } else {
+            ph_recover(kBig<N> ? nullptr : &ops, ri[0], uf, beta, sf, sX, ax);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) { zl[j] = lo_of(j); zh[j] = hi_of(j); zrr[j] = rr[j]; zri[j] = ri[j]; }
+          }
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
             const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
-            const double tt = zr + ri[j] * y[j];
-            const double zn = fmin(fmax(tt, lo_of(j)), hi_of(j));  // osqp project: c_min(c_max(tt, l), u)
-            const double d = rr[j] * (zr - zn);
+            const double tt = zr + zri[j] * y[j];
+            const double zn = fmin(fmax(tt, zl[j]), zh[j]);  // osqp project: c_min(c_max(tt, l), u)
+            const double d = zrr[j] * (zr - zn);
             if constexpr (DELTA) dyv[j] = d;
             y[j] = y[j] + d;
             z[j] = zn;
@@ -2230,6 +2316,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             if (rn > rho_s * p.adaptive_rho_tolerance || rn < rho_s / p.adaptive_rho_tolerance) {
               rho_s = rn;
               set_rho();
+              zc_store();
               refactor = true;
               ++n_upd;
               ++iter;

@@ -37,10 +37,13 @@ struct LaunchArgs {
 
 // Doubles of engine workspace per instance: 0 up to 32 stages (everything in LDS);
 // beyond, a 288-double pad, S^{-1} (N x 144 + 2), F W (N x 72), R^{-1} Q (N x 36),
-// a zero block (72) and, beyond 49 stages, the scaled constraint values (126 N - 18,
-// rounded up to even); the F W block stays reserved (F W lives in LDS since round 3)
+// a zero block (72), beyond 49 stages the scaled constraint values (126 N - 18,
+// rounded up to even), beyond 48 every lane's row of F_k (12 x 16 x the stage rows, N
+// rounded up to 4); the F W block stays reserved (F W lives in LDS since round 3)
 constexpr int64_t work_doubles(int N) {
-  return N > 32 ? 288 + (int64_t)N * (144 + 72 + 36) + 2 + 72 + (N > 49 ? ((126 * N - 18 + 1) & ~1) : 0) : 0;
+  return N > 32 ? 288 + (int64_t)N * (144 + 72 + 36) + 2 + 72 + (N > 49 ? ((126 * N - 18 + 1) & ~1) : 0) +
+                      (N > 48 ? (int64_t)12 * 16 * ((N + 3) & ~3) : 0)
+                : 0;
 }
 
 // Planner launch (mpcq_planner.hip); layouts in include/mpcq.h (mpcq_plan_batch).

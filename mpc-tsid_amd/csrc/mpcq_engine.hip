@@ -570,7 +570,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
   using wcd = std::conditional_t<BIG, const double, lds_cd>;
   using wdd = std::conditional_t<BIG, double, lds_d>;
   wcd* SmR;
-  double* FRg = nullptr;  // (N > 32) this lane's F_k row in the workspace, stride 16 kRows
+  double* FRg = nullptr;  // (kFrWork: N > 48) this lane's F_k row in the workspace, stride 16 kRows
   lds_cd* FWr;
   wcd* QLr;
   wdd* SmW;
@@ -582,7 +582,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     SmW = wk + Work<N>::SM;
     FWW = (lds_d*)&sh.FWs[0][0];  // (Work<N>::FW stays reserved, unused)
     QLW = wk + Work<N>::QL;
-    FRg = wk + Work<N>::FR + t;
+    if (SOLVE) FRg = wk + Work<N>::FR + t;
     zFW = (int)(sh.zero - &sh.FWs[0][0]);
     zQL = Work<N>::ZERO - Work<N>::QL;
     if (SOLVE && t < 72) wk[Work<N>::ZERO + t] = 0.0;

@@ -1899,7 +1899,13 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               if (j + 2 <= MID) {
                 b0 = rhs(j + 2)[0]; b1 = rhs(j + 2)[12 * N];
               }
-              const double yb = hi ? dppd<0x12A>(y) : y;  // row_ror:10: lane q <- lane q + 6
+              // row_ror:10 (lane q <- lane q + 6) on every lane, then a select: as a select on
+              // the rotated value the compiler kept an exec-masked branch, and the register
+              // copies in front of it waited for the right-hand-side loads just issued (an LDS
+              // round trip per step)
+              double yr = dppd<0x12A>(y);
+              asm volatile("" : "+v"(yr));
+              const double yb = hi ? yr : y;
               if (j <= MID) {
                 // y of stage kk(j) (the meeting stage's y_m / v_m stay in registers); the
                 // bottom chain keeps its v_m through the steps past BOT
@@ -1962,7 +1968,9 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               asm volatile("" : : : "memory");
               const double x = pair_sum32(bdot6(gc, xp, bc));  // x = w - G' x_next with -G stored
               if (j < MID) {
-                xp = hi ? dppd<0x12A>(x) : x;
+                double xr = dppd<0x12A>(x);
+                asm volatile("" : "+v"(xr));
+                xp = hi ? xr : x;
                 Xb[12 * (MID - j)] = x;
               } else if constexpr (N & 1) {
                 *Xb = x;

@@ -1232,13 +1232,43 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       for (int i = 0; i < 10; ++i) A[i] = Ab[fo + i];
       return colF_c(A, v);
     };
-    // max over a 16-lane row: quad xor 1, xor 2, then rotations by 4 and 8
-    auto row_max = [](double v) __attribute__((always_inline)) {
-      v = fmax(v, dppd<0xB1>(v));
-      v = fmax(v, dppd<0x4E>(v));
-      v = fmax(v, dppd<0x124>(v));
-      v = fmax(v, dppd<0x128>(v));
-      return v;
+    // Row maxima of several quantities at once, by a transposing butterfly over the
+    // 16-lane row: each step pairs lane s with a partner that differs in one bit
+    // (row_mirror: s ^ 15, bit 3; row_half_mirror: s ^ 7, bit 2; quad xor 2, bit 1;
+    // quad xor 1, bit 0) and the lanes on either side of that bit keep half of the
+    // quantities, so a step reduces half as many values as the one before instead of
+    // every quantity taking all four steps (12 quantities: 13 maxima / DPP moves
+    // instead of 48, plus 13 two-way selects instead of 12).  Maxima are exact in any
+    // order: the results are the ones the per-quantity reduction gave.
+    // one step: lanes with the bit clear keep quantity a, the others b
+    auto tstep = [](auto ctrl, double a, double b, bool hi) __attribute__((always_inline)) {
+      constexpr int C = decltype(ctrl)::value;
+      const double mine = hi ? b : a, send = hi ? a : b;
+      return fmax(mine, dppd<C>(send));
+    };
+    auto sstep = [](auto ctrl, double a) __attribute__((always_inline)) {
+      constexpr int C = decltype(ctrl)::value;
+      return fmax(a, dppd<C>(a));
+    };
+    using kMirror = std::integral_constant<int, 0x140>;   // row_mirror (s ^ 15)
+    using kHalfMir = std::integral_constant<int, 0x141>;  // row_half_mirror (s ^ 7)
+    using kXor2 = std::integral_constant<int, 0x4E>;      // quad_perm [2,3,0,1]
+    using kXor1 = std::integral_constant<int, 0xB1>;      // quad_perm [1,0,3,2]
+    // six quantities over bits 3, 2, 1: lane s keeps quantity 3 b3 + (b2 ? 2 : b1),
+    // maximised over the eight lanes s ^ {0, 15, 7, 8, 2, 13, 5, 10}
+    auto tred6 = [&](const double (&v)[6], int s_) __attribute__((always_inline)) {
+      const bool h3 = s_ & 8, h2 = s_ & 4, h1 = s_ & 2;
+      const double a0 = tstep(kMirror{}, v[0], v[3], h3), a1 = tstep(kMirror{}, v[1], v[4], h3),
+                   a2 = tstep(kMirror{}, v[2], v[5], h3);
+      const double c0 = tstep(kHalfMir{}, a0, a2, h2), c1 = tstep(kHalfMir{}, a1, a2, h2);
+      return tstep(kXor2{}, c0, c1, h1);
+    };
+    // three quantities over the whole row: lane s keeps x0 on lanes 0..3, x1 on 4..7,
+    // x2 on 8..15
+    auto tred3 = [&](double x0, double x1, double x2, int s_) __attribute__((always_inline)) {
+      const bool h3 = s_ & 8, h2 = s_ & 4;
+      const double a0 = tstep(kMirror{}, x0, x2, h3), a1 = tstep(kMirror{}, x1, x2, h3);
+      return sstep(kXor1{}, sstep(kXor2{}, tstep(kHalfMir{}, a0, a1, h2)));
     };
     // A v on the own rows for own-column values (vf, vX), the previous stage's states in P
     auto rowA = [&](double vf, double vX, lds_cd* P, double (&ax)[3]) __attribute__((always_inline)) {
@@ -1302,7 +1332,8 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     // from them is hoisted out of the loop either; cached scratch loads, not volatile
     // ones, which would bypass the caches).  Values and rounding are the ones the check
     // computed before (1.0 / Df etc.).
-    enum { CK_DF, CK_DX, CK_DFI, CK_DXI, CK_EI0, CK_EI1, CK_EI2, CK_PBF, CK_PBX, CK_C, CK_CI, CK_COUNT };
+    enum { CK_DF, CK_DX, CK_DFI, CK_DXI, CK_EI0, CK_EI1, CK_EI2, CK_PBF, CK_PBX, CK_C, CK_CI, CK_E0, CK_E1, CK_E2,
+           CK_BND, CK_COUNT };
     double ck_mem_[CK_COUNT];
     auto ck_ptr = [&]() __attribute__((always_inline)) -> pdbl* {
       pdbl* q = (pdbl*)&ck_mem_[0];
@@ -1325,10 +1356,26 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           case CK_PBF: return Pbf();
           case CK_PBX: return PbX();
           case CK_C: return cscale;
-          default: return 1.0 / cscale;
+          case CK_CI: return 1.0 / cscale;
+          case CK_E0: return E[0];
+          case CK_E1: return E[1];
+          case CK_E2: return E[2];
+          default: return bnd;
         }
       } else {
         return ck_ptr()[i];
+      }
+    };
+    // every constant of the block through one laundered pointer (one batch of loads; the
+    // unused ones are dropped by the compiler)
+    auto ck_all = [&](double (&cv)[CK_COUNT]) __attribute__((always_inline)) {
+      if constexpr (BIG) {
+#pragma unroll
+        for (int i = 0; i < CK_COUNT; ++i) cv[i] = ck(i);
+      } else {
+        const pdbl* const q = ck_ptr();
+#pragma unroll
+        for (int i = 0; i < CK_COUNT; ++i) cv[i] = q[i];
       }
     };
     // The check's lane ids, re-derived from a laundered thread index: the red[] addresses
@@ -1337,12 +1384,44 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
   int tl_ = t;                                                     \
   asm volatile("" : "+v"(tl_));                                    \
   [[maybe_unused]] const int wv = tl_ >> 6, lane = tl_ & 63, s = tl_ & 15
+    // The bounds as the check sees them: lo_of / hi_of from the row scaling E and the
+    // dynamics bound in the check's constant block (ck, read with the others in one
+    // batch).  Formed from the loop's own E / bnd, the products (-inf E, -fz_max E) were
+    // hoisted out of the ADMM loop and spilled, and each came back in the check as a
+    // scratch reload waited for on its own.  Same expressions, same values.
+    auto chk_bounds = [&](const double (&cv)[CK_COUNT], double (&lo)[3], double (&hi)[3])
+        __attribute__((always_inline)) {
+      if constexpr (FUSED) {
+        const double e0 = cv[CK_E0], e1 = cv[CK_E1], e2 = cv[CK_E2], bd = cv[CK_BND];
+        double fz = p.fz_max;
+        asm volatile("" : "+v"(fz));
+        lo[0] = cl ? bd : -kInf * e0;
+        lo[1] = cl ? 0.0 : -fz * e1;
+        lo[2] = cl ? -kInf * e2 : -kInf;
+        hi[0] = cl ? bd : 0.0;
+        hi[1] = 0.0;
+        hi[2] = cl ? 0.0 : kInf;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) { lo[j] = lo_of(j); hi[j] = hi_of(j); }
+      }
+    };
+    // the infeasibility tolerances, laundered for the same reason (10 eps, hoisted, was
+    // spilled)
+    auto chk_eps = [&](double& epi0, double& edi0) __attribute__((always_inline)) {
+      epi0 = p.eps_prim_inf;
+      edi0 = p.eps_dual_inf;
+      asm volatile("" : "+v"(epi0), "+v"(edi0));
+    };
     double dyp[3];     // delta_y projected onto the polar of the recession cone of [l, u]
     auto infeas_cheap = [&](const double (&dy)[3], double dxf, double dxX) __attribute__((always_inline)) {
       MPCQ_CHECK_IDS();
+      double cv[CK_COUNT], lob[3], hib[3];
+      ck_all(cv);
+      chk_bounds(cv, lob, hib);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        const bool uinf = hi_of(j) > kInf * kMinScaling, linf = lo_of(j) < -kInf * kMinScaling;
+        const bool uinf = hib[j] > kInf * kMinScaling, linf = lob[j] < -kInf * kMinScaling;
         dyp[j] = uinf ? (linf ? 0.0 : fmin(dy[j], 0.0)) : (linf ? fmax(dy[j], 0.0) : dy[j]);
       }
       // published together with update_info's states / duals, one barrier for both
@@ -1355,28 +1434,23 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       double ndy = 0.0, ineq = 0.0;
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        const double lj = lo_of(j), hj = hi_of(j);
-        ndy = fmax(ndy, fabs(E[j] * dyp[j]));
+        const double lj = lob[j], hj = hib[j];
+        ndy = fmax(ndy, fabs(cv[CK_E0 + j] * dyp[j]));
         ineq += hj * fmax(dyp[j], 0.0) + lj * fmin(dyp[j], 0.0);
       }
       if (phantom) ineq = 0.0;  // a sum: stage N-1 counts once
       double q3[2] = {0.0, 0.0};
       {
-        const double df = ck(CK_DF), dx = ck(CK_DX), dif = ck(CK_DFI), diX = ck(CK_DXI);
-        const double pbf = ck(CK_PBF), pbx = ck(CK_PBX);
+        const double df = cv[CK_DF], dx = cv[CK_DX], dif = cv[CK_DFI], diX = cv[CK_DXI];
+        const double pbf = cv[CK_PBF], pbx = cv[CK_PBX];
         if (cl) {
           q3[0] = fmax(fabs(df * dxf), fabs(dx * dxX));                // ||D dx||
           q3[1] = fmax(fabs(pbf * dxf * dif), fabs(pbx * dxX * diX));  // ||D^-1 P dx||
         }
       }
-      // maxima over the wave (lanes 0, 2, 3 keep quantity s), the sum by xor butterflies
-      double mx[3] = {ndy, q3[0], q3[1]}, mine = 0.0;
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        const double v = row_max(mx[e]);
-        mine = s == (e == 0 ? 0 : e + 1) ? v : mine;
-      }
-      mine = pair_max(row_pair_max(mine));
+      // maxima over the wave (lanes 0 / 4 / 8 keep ||E dy|| / ||D dx|| / ||D^-1 P dx||,
+      // published in slots 0 / 2 / 3), the sum by xor butterflies
+      const double mine = pair_max(row_pair_max(tred3(ndy, q3[0], q3[1], s)));
       ineq += dppd<0xB1>(ineq);
       ineq += dppd<0x4E>(ineq);
       ineq += dppd<0x124>(ineq);
@@ -1389,7 +1463,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         ineq = __longlong_as_double(((long long)hi_[0] << 32) | lo_[0]) +
                __longlong_as_double(((long long)hi_[1] << 32) | lo_[1]);
       }
-      if (lane == 0 || lane == 2 || lane == 3) sh.red[32 * wv + 16 + lane] = mine;
+      if (lane == 0 || lane == 4 || lane == 8) sh.red[32 * wv + 16 + (lane == 0 ? 0 : 2 + (lane >> 3))] = mine;
       if (lane == 6) sh.red[32 * wv + 16 + 6] = ineq;
       sync_all();  // (update_info(INF) relies on this barrier for its own publication)
     };
@@ -1398,13 +1472,16 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     auto infeas_products = [&](double dxf, double dxX) __attribute__((always_inline)) {
       MPCQ_CHECK_IDS();
       launder_p();
+      double cv[CK_COUNT];
+      ck_all(cv);
       double vu = -INFINITY, vl = -INFINITY;
       {
-        double adx[3];
+        double adx[3], lob[3], hib[3];
         rowA(dxf, dxX, (lds_cd*)&sh.u.it.na[0][0], adx);
+        chk_bounds(cv, lob, hib);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          const double lj = lo_of(j), hj = hi_of(j), v = adx[j] / E[j];
+          const double lj = lob[j], hj = hib[j], v = adx[j] / cv[CK_E0 + j];
           if (hj < kInf * kMinScaling) vu = fmax(vu, v);
           if (lj > -kInf * kMinScaling) vl = fmax(vl, -v);
         }
@@ -1413,17 +1490,12 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       {
         double dtf, dtX;
         colAt(dyp, &sh.u.it.nb[0][0], dtf, dtX);
-        const double dif = ck(CK_DFI), diX = ck(CK_DXI);
+        const double dif = cv[CK_DFI], diX = cv[CK_DXI];
         if (cl) naty = fmax(fabs(dtf * dif), fabs(dtX * diX));  // ||D^-1 A' dy||
       }
-      double mx[3] = {naty, vu, vl}, mine = 0.0;
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        const double v = row_max(mx[e]);
-        mine = s == (e == 0 ? 1 : e + 3) ? v : mine;
-      }
-      mine = pair_max(row_pair_max(mine));
-      if (lane == 1 || lane == 4 || lane == 5) sh.red[32 * wv + 16 + lane] = mine;
+      // lanes 0 / 4 / 8 keep ||D^-1 A' dy|| / vu / vl, published in slots 1 / 4 / 5
+      const double mine = pair_max(row_pair_max(tred3(naty, vu, vl, s)));
+      if (lane == 0 || lane == 4 || lane == 8) sh.red[32 * wv + 16 + (lane == 0 ? 1 : 4 + (lane >> 3))] = mine;
       sync_all();
       const int e = s < 6 ? s : 0;  // slots 16..21 are all maxima (0 / 2 / 3 from infeas_cheap)
       double v = sh.red[16 + e];
@@ -1431,10 +1503,12 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       for (int w = 1; w < NW; ++w) v = fmax(v, sh.red[32 * w + 16 + e]);
       const double ndy = rbc<0>(v), ndx = rbc<2>(v);  // (the cheap maxima, kept in slots 0 / 2)
       const double naty_ = rbc<1>(v), vu_ = rbc<4>(v), vl_ = rbc<5>(v);
+      double epi0, edi0;
+      chk_eps(epi0, edi0);
       int bits = 0;
 #pragma unroll
       for (int fi = 0; fi < 2; ++fi) {
-        const double f = fi == 0 ? 1.0 : 10.0, epi = f * p.eps_prim_inf, edi = f * p.eps_dual_inf;
+        const double f = fi == 0 ? 1.0 : 10.0, epi = f * epi0, edi = f * edi0;
         const bool pi = ((inf_need >> (2 * fi)) & 1) && naty_ < epi * ndy;
         const bool di = ((inf_need >> (2 * fi)) & 2) && !(vu_ > edi * ndx) && !(vl_ > edi * ndx);
         bits |= (pi ? 1 : 0) << (2 * fi);
@@ -1462,7 +1536,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       const double dif = ck(CK_DFI), diX = ck(CK_DXI), pbf = ck(CK_PBF), pbx = ck(CK_PBX);
       const double cinv = ck(CK_CI), csc = ck(CK_C);
       lds_cd* const YV = (lds_cd*)&sh.u.it.yv[0][0];  // X_{k'} of stage k' >= 1 at 12 (k' - 1)
-      double mine = 0.0;                              // this lane's row maximum (quantity s)
+      double mine, pmine;  // this lane's row maxima (tred6: primal quantity 3 b3 + (b2 ? 2 : b1))
       {  // primal side: A x - z on the own rows
         double ax[3], q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         rowA(xf, xX, YV, ax);
@@ -1476,11 +1550,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           q6[4] = fmax(q6[4], fabs(ax[j]));
           q6[5] = fmax(q6[5], fabs(z[j]));
         }
-#pragma unroll
-        for (int e = 0; e < 6; ++e) {
-          const double v = row_max(q6[e]);
-          mine = s == e ? v : mine;
-        }
+        pmine = tred6(q6, s);
       }
       STAMP(5);
       {  // dual side: P x + A' y on the own columns
@@ -1497,23 +1567,23 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           q6[4] = fmax(fabs(pxf), fabs(pxX));
           q6[5] = fmax(fabs(atf), fabs(atX));
         }
-#pragma unroll
-        for (int e = 0; e < 6; ++e) {
-          const double v = row_max(q6[e]);
-          mine = s == 6 + e ? v : mine;
-        }
+        // the last step of the butterfly joins the sides: primal quantity e on lane
+        // 2 e (e < 3) / 2 e + 2 (e >= 3), the dual's on the lane after it
+        mine = tstep(kXor1{}, pmine, tred6(q6, s), s & 1);
       }
       mine = pair_max(row_pair_max(mine));  // the wave's four rows
-      if (lane < 12) sh.red[32 * wv + lane] = mine;
+      if (lane < 16) sh.red[32 * wv + lane] = mine;
       sync_all();
       STAMP(8);
       double qv[12];
       {
-        const int e = s < 12 ? s : 0;
-        double v = sh.red[e];
+        double v = sh.red[s];
 #pragma unroll
-        for (int w = 1; w < NW; ++w) v = fmax(v, sh.red[32 * w + e]);
-        gather_direct12(v, qv);
+        for (int w = 1; w < NW; ++w) v = fmax(v, sh.red[32 * w + s]);
+        qv[0] = rbc<0>(v); qv[1] = rbc<2>(v); qv[2] = rbc<4>(v);
+        qv[3] = rbc<8>(v); qv[4] = rbc<10>(v); qv[5] = rbc<12>(v);
+        qv[6] = rbc<1>(v); qv[7] = rbc<3>(v); qv[8] = rbc<5>(v);
+        qv[9] = rbc<9>(v); qv[10] = rbc<11>(v); qv[11] = rbc<13>(v);
       }
       pri_res = qv[0];
       dua_res = cinv * qv[6];
@@ -1538,10 +1608,12 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         // int at the end: SGPRs here would push loop-carried scalars into VGPR lanes
         // (v_readlane on the hot path, measured)
         const double ndy = rbc<0>(v), ndx = rbc<2>(v), npdx = rbc<3>(v), ineq = rbc<6>(v);
+        double epi0, edi0;
+        chk_eps(epi0, edi0);
         int need = 0;
 #pragma unroll
         for (int fi = 0; fi < 2; ++fi) {
-          const double f = fi == 0 ? 1.0 : 10.0, epi = f * p.eps_prim_inf, edi = f * p.eps_dual_inf;
+          const double f = fi == 0 ? 1.0 : 10.0, epi = f * epi0, edi = f * edi0;
           const bool pi = !(pri_res < f * eps_pri) && ndy > kDivTol && ineq < epi * ndy;
           const bool di = !(dua_res < f * eps_dua) && ndx > kDivTol && 0.0 < csc * edi * ndx &&
                           npdx < csc * edi * ndx;
@@ -1681,6 +1753,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         q[CK_DF] = Df; q[CK_DX] = DX; q[CK_DFI] = 1.0 / Df; q[CK_DXI] = 1.0 / DX;
         q[CK_EI0] = 1.0 / E[0]; q[CK_EI1] = 1.0 / E[1]; q[CK_EI2] = 1.0 / E[2];
         q[CK_PBF] = Pbf(); q[CK_PBX] = PbX(); q[CK_C] = cscale; q[CK_CI] = 1.0 / cscale;
+        q[CK_E0] = E[0]; q[CK_E1] = E[1]; q[CK_E2] = E[2]; q[CK_BND] = bnd;
       }
       // warm start (osqp_warm_start: x = D^-1 x0, z = A x; y = c E^-1 y0)
       if (a.warm_x) {

@@ -2,8 +2,8 @@
 # Build an experiment variant of the engine for timing (tools/iterbench.py):
 #   bash tools/build_variant.sh <name> <engine source> [extra hipcc flags]
 # -> mpc-tsid_amd/csrc/build/variants/libmpcq_<name>.so (loaded with
-#    MPCQ_LIB_VARIANT=exp:<name>); horizons $VARIANT_HORIZONS (default 16 32) from
-#    the variant source, the rest of the library from the current objects (run
+#    MPCQ_LIB_VARIANT=exp:<name>); only the horizons $VARIANT_HORIZONS (default 16 32),
+#    from the variant source, the rest of the library from the current objects (run
 #    make first).
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -18,11 +18,13 @@ for n in $HS; do
   J=$((J + 1)); if [ $((J % 8)) -eq 0 ]; then wait; fi
 done
 wait
-# the other horizons from the production objects
+# only the variant's horizons (a dispatch unit restricted to them: the library stays
+# small, every gpurun call ships it)
 OBJS=""
-for n in $(seq 4 64); do
-  if [[ " $HS " == *" $n "* ]]; then OBJS="$OBJS $OUT/$NAME/e$n.o"; else OBJS="$OBJS $C/build/engine_n$n.o"; fi
-done
+HX=""
+for n in $HS; do OBJS="$OBJS $OUT/$NAME/e$n.o"; HX="$HX X($n)"; done
+printf '#include "mpcq_internal.h"\n#undef MPCQ_HORIZONS\n#define MPCQ_HORIZONS(X) %s\n#include "mpcq_dispatch.cpp"\n' "$HX" > $OUT/$NAME/dispatch.cpp
+/opt/rocm/bin/hipcc $F -I$R/include -c -o $OUT/$NAME/dispatch.o $OUT/$NAME/dispatch.cpp
 /opt/rocm/bin/hipcc $F -shared -o $OUT/libmpcq_$NAME.so $OBJS $C/build/mpcq_planner.o $C/build/mpcq_session.o \
-  $C/build/mpcq_api.o $C/build/mpcq_dispatch.o
+  $C/build/mpcq_api.o $OUT/$NAME/dispatch.o
 echo "built $OUT/libmpcq_$NAME.so"

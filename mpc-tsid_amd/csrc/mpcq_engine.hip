@@ -1237,9 +1237,9 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     // (row_mirror: s ^ 15, bit 3; row_half_mirror: s ^ 7, bit 2; quad xor 2, bit 1;
     // quad xor 1, bit 0) and the lanes on either side of that bit keep half of the
     // quantities, so a step reduces half as many values as the one before instead of
-    // every quantity taking all four steps (12 quantities: 13 maxima / DPP moves
-    // instead of 48, plus 13 two-way selects instead of 12).  Maxima are exact in any
-    // order: the results are the ones the per-quantity reduction gave.
+    // every quantity taking all four steps (12 quantities: 13 maxima and 13 DPP moves
+    // instead of 48 each, for 26 two-way selects instead of 12).  Maxima are exact in
+    // any order: the results are the ones the per-quantity reduction gave.
     // one step: lanes with the bit clear keep quantity a, the others b
     auto tstep = [](auto ctrl, double a, double b, bool hi) __attribute__((always_inline)) {
       constexpr int C = decltype(ctrl)::value;

@@ -1414,10 +1414,11 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       asm volatile("" : "+v"(epi0), "+v"(edi0));
     };
     double dyp[3];     // delta_y projected onto the polar of the recession cone of [l, u]
-    auto infeas_cheap = [&](const double (&dy)[3], double dxf, double dxX) __attribute__((always_inline)) {
+    // cv: the constant block, read by the caller ahead of the check (ck_all)
+    auto infeas_cheap = [&](const double (&dy)[3], double dxf, double dxX, const double (&cv)[CK_COUNT])
+        __attribute__((always_inline)) {
       MPCQ_CHECK_IDS();
-      double cv[CK_COUNT], lob[3], hib[3];
-      ck_all(cv);
+      double lob[3], hib[3];
       chk_bounds(cv, lob, hib);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
@@ -2320,7 +2321,8 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         // their own without them, so the check / infeasibility code and its live values
         // sit outside the hot loop's register allocation (inside it, they cost 0.31 us
         // per iteration through spills on the sweep path, measured).
-        auto admm_iter = [&](auto delta_tag, const RhsOps& ops, double (&dyv)[3], double& dxf_, double& dxX_)
+        auto admm_iter = [&](auto delta_tag, const RhsOps& ops, double (&dyv)[3], double& dxf_, double& dxX_,
+                             double (&cvp)[CK_COUNT])
             __attribute__((always_inline)) {
           constexpr bool DELTA = decltype(delta_tag)::value;
           double uf, beta, sf, sX, ax[3];
@@ -2329,6 +2331,9 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // per lane, 17.68 -> 16.75 us per iteration, profiles/r03c_iterbench.txt)
           ph_rhs(true, kBig<N> ? nullptr : &ops, kNoW, 0.0, 0.0, uf, beta);
           ph_sweep();
+          // DELTA (the last iteration before a check): the check's constant block is read
+          // here, its memory latency behind the force recovery and the z / y / x update
+          if constexpr (DELTA) ck_all(cvp);
           double zl[3], zh[3], zrr[3], zri[3];  // the update's per-row constants
           if constexpr (kZcMem<N>) {
             ph_recover(nullptr, zc_ptr()[ZC_RI], uf, beta, sf, sX, ax);
@@ -2371,9 +2376,10 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // for them in the loop
           RhsOps ops;
           if constexpr (!kBig<N>) load_rhs_ops(ops);
+          double cvp[CK_COUNT];
 #pragma nounroll
-          for (int r_ = 1; r_ < until; ++r_, ++iter) admm_iter(std::false_type{}, ops, dyv, dxf_, dxX_);
-          admm_iter(std::true_type{}, ops, dyv, dxf_, dxX_);
+          for (int r_ = 1; r_ < until; ++r_, ++iter) admm_iter(std::false_type{}, ops, dyv, dxf_, dxX_, cvp);
+          admm_iter(std::true_type{}, ops, dyv, dxf_, dxX_, cvp);
           // iter % check_termination == 0 / iter % adaptive_rho_interval == 0, by countdown
           const bool can_check = chk_on && (to_check -= until) == 0;
           if (can_check) to_check = p.check_termination;
@@ -2382,7 +2388,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           last_checked = can_check;
           // the last iteration's information is always formed here, while its deltas are
           // live (osqp's update_info after the loop when the last iteration was unchecked)
-          infeas_cheap(dyv, dxf_, dxX_);
+          infeas_cheap(dyv, dxf_, dxX_, cvp);
           update_info(std::true_type{});
           if (inf_need) infeas_products(dxf_, dxX_);
           if (!(isfinite(pri_res) && isfinite(dua_res))) { status = MPCQ_STATUS_NONFINITE; break; }

@@ -1470,11 +1470,9 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     };
     // the products, where a cheap condition holds (inf_need != 0, uniform): A' dy for
     // the primal test, A dx for the dual one, on the deltas infeas_cheap published
-    auto infeas_products = [&](double dxf, double dxX) __attribute__((always_inline)) {
+    auto infeas_products = [&](double dxf, double dxX, const double (&cv)[CK_COUNT]) __attribute__((always_inline)) {
       MPCQ_CHECK_IDS();
       launder_p();
-      double cv[CK_COUNT];
-      ck_all(cv);
       double vu = -INFINITY, vl = -INFINITY;
       {
         double adx[3], lob[3], hib[3];
@@ -1524,7 +1522,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     // permlane swaps and over the waves through red[].  INF: also combine the
     // cheap partials of infeas_cheap into inf_need.
     // INF: after infeas_cheap, which has published the states / duals with its deltas
-    auto update_info = [&](auto inf_tag) __attribute__((always_inline)) {
+    auto update_info = [&](auto inf_tag, const double (&cv)[CK_COUNT]) __attribute__((always_inline)) {
       constexpr bool INF = decltype(inf_tag)::value;
       MPCQ_CHECK_IDS();
       if constexpr (!INF) {
@@ -1533,9 +1531,9 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       }
       STAMP(4);
       launder_p();
-      const double ei3[3] = {ck(CK_EI0), ck(CK_EI1), ck(CK_EI2)};
-      const double dif = ck(CK_DFI), diX = ck(CK_DXI), pbf = ck(CK_PBF), pbx = ck(CK_PBX);
-      const double cinv = ck(CK_CI), csc = ck(CK_C);
+      const double ei3[3] = {cv[CK_EI0], cv[CK_EI1], cv[CK_EI2]};
+      const double dif = cv[CK_DFI], diX = cv[CK_DXI], pbf = cv[CK_PBF], pbx = cv[CK_PBX];
+      const double cinv = cv[CK_CI], csc = cv[CK_C];
       lds_cd* const YV = (lds_cd*)&sh.u.it.yv[0][0];  // X_{k'} of stage k' >= 1 at 12 (k' - 1)
       double mine, pmine;  // this lane's row maxima (tred6: primal quantity 3 b3 + (b2 ? 2 : b1))
       {  // primal side: A x - z on the own rows
@@ -2389,8 +2387,8 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // the last iteration's information is always formed here, while its deltas are
           // live (osqp's update_info after the loop when the last iteration was unchecked)
           infeas_cheap(dyv, dxf_, dxX_, cvp);
-          update_info(std::true_type{});
-          if (inf_need) infeas_products(dxf_, dxX_);
+          update_info(std::true_type{}, cvp);
+          if (inf_need) infeas_products(dxf_, dxX_, cvp);
           if (!(isfinite(pri_res) && isfinite(dua_res))) { status = MPCQ_STATUS_NONFINITE; break; }
           if (can_check) {  // osqp check_termination
             if (converged(1.0)) { status = MPCQ_STATUS_SOLVED; break; }
@@ -2572,7 +2570,11 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
                   printf("blk0 k %d s %d j %d row %d act %d bred %.3e ax %.6e yp %.3e -> z %.6e y %.3e lo %.3e hi %.3e\n",
                          k, s, j, nat_row(j), act[j], bred[j], axp[j], yp[j], z[j], y[j], lo_of(j), hi_of(j));
 #endif
-            update_info(std::false_type{});
+            {
+              double cvq[CK_COUNT];
+              ck_all(cvq);
+              update_info(std::false_type{}, cvq);
+            }
 #ifdef MPCQ_DEBUG_POLISH
             if (b < 2 && t == 0) printf("blk %d rd %d admm pri %.3e dua %.3e | polished pri %.3e dua %.3e eps %.3e %.3e\n", (int)b, rd, a_pri, a_dua, pri_res, dua_res, eps_pri, eps_dua);
 #endif

@@ -1,6 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-# r03zz: the round's final build -- GPU suite, smoke, every bench line, the rocprof passes
-timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/r03zz_pytest_gpu.log 2>&1 &&
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03zz_smoke.log 2>&1 &&
-bash tools/bench_all.sh r03zz
+# r03zy: the round's final build -- GPU suite, smoke, every bench line, the rocprof passes
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/r03zy_pytest_gpu.log 2>&1 &&
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03zy_smoke.log 2>&1 &&
+bash tools/bench_all.sh r03zy

@@ -33,7 +33,11 @@
 extern "C" {
 #endif
 
-#define MPCQ_ABI_VERSION 2  /* 2: eps_prim_inf / eps_dual_inf, dual_warm, infeasibility statuses */
+/* ABI changelog:
+ *   2: eps_prim_inf / eps_dual_inf, dual_warm, infeasibility statuses
+ *   3: info[b][3] = the ADMM's own exit status (before polish; was always 0),
+ *      MPCQ_SV_ORDER added (MPCQ_SV_COUNT 16 -> 17), initialised to the identity */
+#define MPCQ_ABI_VERSION 3
 
 /* error codes (return values) */
 #define MPCQ_OK 0
@@ -288,14 +292,17 @@ int mpcq_session_tick(mpcq_session* s, int k, const double* state, const double*
 #define MPCQ_SV_ROT_FLAG 14 /* [B] int32 */
 #define MPCQ_SV_H_ROT 15    /* [B] */
 #define MPCQ_SV_ORDER 16    /* [B] int32: the next tick's dispatch order (read-only: a permutation of
-                               0..B-1, longest previous solve first, buckets of 16 iterations) */
+                               0..B-1, longest previous solve first, buckets of 16 iterations; the
+                               identity until the first tick) */
 #define MPCQ_SV_COUNT 17
 /* Copy array `what` to dst (host, or device with MPCQ_FLAG_DEVICE_PTRS); blocking. */
 int mpcq_session_read(mpcq_session* s, int what, void* dst, uint32_t flags);
 /* Overwrite array `what` from src (host, or device with MPCQ_FLAG_DEVICE_PTRS); blocking.
  * MPCQ_SV_ORDER is read-only (MPCQ_E_INVALID). */
 int mpcq_session_write(mpcq_session* s, int what, const void* src, uint32_t flags);
-/* Device address of array `what` (valid until mpcq_session_destroy). */
+/* Device address of array `what` (valid until mpcq_session_destroy).  The engine reads
+ * MPCQ_SV_ORDER as its workgroup -> robot map: writing through its device address is not
+ * allowed (a non-permutation would solve some robots twice and others not at all). */
 int mpcq_session_device_ptr(mpcq_session* s, int what, void** out);
 
 /* ---- diagnostics -----------------------------------------------------------

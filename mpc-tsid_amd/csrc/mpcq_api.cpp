@@ -122,8 +122,9 @@ int ensure_work(mpcq_ctx* c, int64_t B, double** out) {
       c->work = nullptr;
       return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) for the engine workspace failed", bytes);
     }
-    // zeroed once: like the LDS sweep arrays, the padding slots the sweeps over-read
-    // must not hold NaN (a zero factor does not cancel it)
+    // zeroed once, as a guard only: no kernel reads a workspace slot it has not
+    // written earlier in the same launch (DESIGN.md §4.1 "LDS hygiene"; the suite
+    // passes on a build without the LDS zeroing either)
     HIP_TRY(hipMemsetAsync(c->work, 0, bytes, c->stream));
     c->work_bytes = bytes;
   }
@@ -672,6 +673,8 @@ int mpcq_session_create(mpcq_ctx* c, int64_t B, const mpcq_planner_params* pp, c
   put(MPCQ_SV_ROT_FLAG, hi);
   put(MPCQ_SV_STATUS, hi);
   put(MPCQ_SV_ITERS, hi);
+  for (int64_t b = 0; b < B; ++b) hi[b] = (int32_t)b;  // a permutation from the start: the identity
+  put(MPCQ_SV_ORDER, hi);
   for (size_t e = 0; e < (size_t)B * 260; ++e) h[e] = NAN;
   put(MPCQ_SV_FSTEPS, h);
   free(h);

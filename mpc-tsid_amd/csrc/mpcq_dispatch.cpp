@@ -7,8 +7,8 @@
 // holds four 16-lane stage rows; N that is not a multiple of 4 runs the rows past
 // N as copies of stage N-1 (kRows in mpcq_engine.hip).  Up to 16 stages two
 // instances share a CU, up to 32 one (LDS, checked by static_asserts in
-// mpcq_engine.hip); beyond 32, S^{-1}, F W and R^{-1} Q live in a per-instance
-// global workspace (work_doubles), beyond 56 the scaled constraint values too.
+// mpcq_engine.hip); beyond 32, S^{-1} and R^{-1} Q live in a per-instance
+// global workspace (work_doubles), beyond 49 the scaled constraint values too (kAbG).
 #include "mpcq_internal.h"
 
 namespace mpcq {

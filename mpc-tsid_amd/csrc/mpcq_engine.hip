@@ -490,7 +490,7 @@ struct Work {  // offsets (doubles) inside one instance's workspace
 
 template <int N>
 struct Smem {
-  double Ab[kAbG<N> ? 2 : 126 * N - 18];  // scaled constraint values, CSC order (N > 56: Work<N>::AB)
+  double Ab[kAbG<N> ? 2 : 126 * N - 18];  // scaled constraint values, CSC order (N > 49: Work<N>::AB)
   // GH[0] = M^{-1}, GH[SIG(k)] = G_k (1 <= k <= m), GH[SIG(k+1)] = H_k (m <= k < N-1),
   // row-major (the sweeps' step order, see SIG).
   // During the factorisation slot k holds Q_k [0,36), F_k W_k [36,108) and the
@@ -558,7 +558,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
   const int64_t b = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;  // the instance
   STAMP_DECL
   constexpr bool BIG = kBig<N>, ABG = kAbG<N>;
-  // the scaled constraint values: LDS, or (N > 56) this instance's workspace (the
+  // the scaled constraint values: LDS, or (N > 49) this instance's workspace (the
   // formulation-only launch builds them straight into its Ax output)
   using acd = std::conditional_t<ABG, const double, lds_cd>;
   double* AbW;

@@ -141,6 +141,7 @@ def build(force: bool = False) -> str:
     return LIB_PATH
 
 
+ABI_VERSION = 3  # include/mpcq.h MPCQ_ABI_VERSION these bindings follow
 _lib = None
 _hip_runtime = None
 
@@ -212,6 +213,9 @@ def lib():
            "mpcq_plan_batch", "mpcq_session_create", "mpcq_session_destroy", "mpcq_session_tick",
            "mpcq_session_read", "mpcq_session_write", "mpcq_session_device_ptr", "mpcq_debug_set_stamps"):
         getattr(L, name).restype = C.c_int
+    if L.mpcq_abi_version() != ABI_VERSION:
+        raise MpcqError(E_UNSUPPORTED, f"{LIB_PATH} has ABI {L.mpcq_abi_version()}, these bindings ABI {ABI_VERSION}: "
+                        f"rebuild it (`make -C {CSRC}`)")
     _lib = L
     return L
 

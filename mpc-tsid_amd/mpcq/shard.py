@@ -7,8 +7,6 @@ rank 0 (RCCL over xGMI on the GPU box, gloo in the CPU tests).
 """
 from __future__ import annotations
 
-import numpy as np
-
 
 def shard_bounds(total: int, world: int, rank: int):
     """Contiguous shard [lo, hi) of rank ``rank``: ceil(total / world) per rank, the last ones short."""
@@ -20,11 +18,12 @@ def shard_bounds(total: int, world: int, rank: int):
 
 
 def shard_batch(total: int, world: int, rank: int, n_steps: int, gaits, seed: int):
-    """This rank's slice of the seeded global synthetic batch (mpcq.synth.make_batch(total, ...))."""
+    """This rank's slice of the seeded global synthetic batch (mpcq.synth.make_batch(total, ...)),
+    generated alone: the batch is seeded per block of synth.CHUNK instances, so a rank
+    builds only the blocks of its own shard."""
     from . import synth
     lo, hi = shard_bounds(total, world, rank)
-    g = synth.make_batch(total, n_steps, gaits=gaits, seed=seed)
-    return {k: (v[lo:hi] if isinstance(v, np.ndarray) and v.shape[:1] == (total,) else v) for k, v in g.items()}
+    return synth.make_batch(total, n_steps, gaits=gaits, seed=seed, lo=lo, hi=hi)
 
 
 def gather_rows(dist, t, total: int, world: int, rank: int):

@@ -182,17 +182,17 @@ def footsteps(gait_tab: np.ndarray, l_feet, v_cur, v_ref, h: float = H_REF) -> n
     return fs
 
 
-def make_batch(batch: int, n_steps: int = 16, gaits=("trot",), seed: int = 0,
-               static: bool = False, interleave: bool = True):
-    """Seeded synthetic batch.
+CHUNK = 1024  # instances per independently seeded block of a synthetic batch
 
-    Returns dict(xref (B,12,N+1), fsteps (B,20,13), gait (B,) int index into
-    ``gaits``, offset (B,) roll offset, v_ref (B,6)).  ``static=True`` gives the
-    C1 case: v_ref = 0, standing state, every instance on the unrolled table.
-    Mixed gaits are interleaved (instance b gets gaits[b % len(gaits)]).
-    """
-    rng = np.random.default_rng(seed)
-    B, N = int(batch), int(n_steps)
+
+def _chunk_rng(seed: int, c: int):
+    """Generator of block c: block 0 is default_rng(seed) itself, so a batch of at
+    most CHUNK instances is the one the earlier rounds generated."""
+    return np.random.default_rng(seed if c == 0 else [seed, c])
+
+
+def _make_block(rng, g0: int, B: int, N: int, gaits, static: bool, interleave: bool):
+    """Instances g0 .. g0 + B - 1 of a batch, drawn from ``rng``."""
     v_ref = np.zeros((B, 6))
     if not static:
         v_ref[:, 0] = rng.uniform(-0.5, 1.0, B)
@@ -212,7 +212,7 @@ def make_batch(batch: int, n_steps: int = 16, gaits=("trot",), seed: int = 0,
     if not static:
         l_feet[:, 0:2, :] += rng.uniform(-0.03, 0.03, (B, 2, 4))
     if interleave:
-        gsel = np.arange(B) % len(gaits)
+        gsel = (g0 + np.arange(B)) % len(gaits)
     else:
         gsel = rng.integers(0, len(gaits), B)
     offset = np.zeros(B, np.int64) if static else rng.integers(0, N, B)
@@ -225,6 +225,39 @@ def make_batch(batch: int, n_steps: int = 16, gaits=("trot",), seed: int = 0,
             tab = rolled_table(gname, N, int(off))
             fsteps[sel] = footsteps(tab, l_feet[sel], v_cur[sel], v_ref[sel])
     return dict(xref=xref, fsteps=fsteps, gait=gsel, offset=offset, v_ref=v_ref)
+
+
+def make_batch(batch: int, n_steps: int = 16, gaits=("trot",), seed: int = 0,
+               static: bool = False, interleave: bool = True, lo: int = 0, hi: int | None = None):
+    """Seeded synthetic batch, or the slice [lo, hi) of it.
+
+    Returns dict(xref (B,12,N+1), fsteps (B,20,13), gait (B,) int index into
+    ``gaits``, offset (B,) roll offset, v_ref (B,6)).  ``static=True`` gives the
+    C1 case: v_ref = 0, standing state, every instance on the unrolled table.
+    Mixed gaits are interleaved (instance b gets gaits[b % len(gaits)]).
+
+    The batch is generated in blocks of CHUNK instances, block c from its own
+    generator (``_chunk_rng(seed, c)``), so a slice costs only the blocks it
+    touches and equals the same rows of the whole batch: a rank of a sharded run
+    builds its own shard only (mpcq/shard.py).
+    """
+    B, N = int(batch), int(n_steps)
+    hi = B if hi is None else int(hi)
+    lo = int(lo)
+    if not 0 <= lo <= hi <= B:
+        raise ValueError(f"slice [{lo}, {hi}) of a batch of {B}")
+    parts = []
+    for c in range(lo // CHUNK, -(-hi // CHUNK)):
+        c0, c1 = c * CHUNK, min((c + 1) * CHUNK, B)
+        blk = _make_block(_chunk_rng(seed, c), c0, c1 - c0, N, gaits, static, interleave)
+        a, b = max(lo, c0) - c0, min(hi, c1) - c0
+        parts.append({k: v[a:b] for k, v in blk.items()})
+    if not parts:
+        blk = _make_block(_chunk_rng(seed, 0), 0, 0, N, gaits, static, interleave)
+        return blk
+    if len(parts) == 1:
+        return parts[0]
+    return {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
 
 
 def motionless(n_steps: int = 16) -> dict:

@@ -44,7 +44,7 @@ def golden_h():
     """Fixtures at the other horizons (gen_golden.py horizons / horizons_r3):
     {N: {field: array}}."""
     out = {}
-    for name in ("golden_horizons.npz", "golden_horizons_r3.npz"):
+    for name in ("golden_horizons.npz", "golden_horizons_r3.npz", "golden_horizons_r4.npz"):
         d = np.load(os.path.join(GOLDEN, name))
         for N in d["horizons"]:
             pre = f"n{int(N)}_"
@@ -54,4 +54,5 @@ def golden_h():
 
 # the horizons the fixtures cover besides 16 / 32: multiples of 4 up to 32, N = 48
 # (round 2), and round 3's non-multiples of 4, odd N and the range up to 64
-FIXTURE_HORIZONS = (4, 5, 6, 8, 10, 12, 13, 20, 24, 28, 33, 36, 40, 48, 57, 64)
+# and round 4's layout switch points 49 (13 waves) and 50 (constraint values in the workspace)
+FIXTURE_HORIZONS = (4, 5, 6, 8, 10, 12, 13, 20, 24, 28, 33, 36, 40, 48, 49, 50, 57, 64)

@@ -5,6 +5,7 @@
                                                  # (N = 4, 8, 12, 20, 24, 28 and 48; keys n<N>_<field>)
     python tests/golden/gen_golden.py horizons_r3  # golden_horizons_r3.npz: N = 5, 6, 10, 13, 33,
                                                    # 36, 40, 57, 64
+    python tests/golden/gen_golden.py horizons_r4  # golden_horizons_r4.npz: N = 49, 50
 
 What it does, per instance:
 1. Inputs: seeded synthetic (xref, fsteps) from mpcq.synth (trot / bound /
@@ -271,9 +272,13 @@ def build(N: int, per_gait: int, seed: int, extra=True):
 HORIZONS = ((4, 2, 404), (8, 4, 808), (12, 2, 1212), (20, 2, 2020), (24, 4, 2424), (28, 2, 2828), (48, 1, 4848))
 # round 3: horizons that are not a multiple of 4 (phantom stage rows), odd ones (the
 # two sweep chains equally long) and the global-workspace range up to n_periods = 4
-# (N = 64; beyond 56 stages the constraint values leave LDS too)
+# (N = 64; beyond 49 stages the constraint values leave LDS too)
 HORIZONS_R3 = ((5, 1, 505), (6, 2, 606), (10, 2, 1010), (13, 1, 1313), (33, 1, 3333), (36, 1, 3636), (40, 1, 4040),
                (57, 1, 5757), (64, 1, 6464))
+# round 4: the layout switch points beyond 48 stages -- N = 49 (13 waves: the F row and
+# the z update's constants leave registers, the constraint values still in LDS) and
+# N = 50 (the constraint values in the workspace, kAbG)
+HORIZONS_R4 = ((49, 1, 4949), (50, 1, 5050))
 
 
 def main_horizons():
@@ -301,7 +306,22 @@ def main_horizons_r3():
     print("wrote", path, os.path.getsize(path), "bytes")
 
 
+def main_horizons_r4():
+    """golden_horizons_r4.npz: HORIZONS_R4, same fields and key scheme as main_horizons."""
+    out = {}
+    for N, per_gait, seed in HORIZONS_R4:
+        arrs = build(N, per_gait, seed)
+        for k, v in arrs.items():
+            out[f"n{N}_{k}"] = v
+    path = os.path.join(HERE, "golden_horizons_r4.npz")
+    np.savez_compressed(path, horizons=np.array([h[0] for h in HORIZONS_R4]), **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "horizons_r4":
+        main_horizons_r4()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "horizons":
         main_horizons()
         return

@@ -37,7 +37,7 @@ def test_exports_every_declared_symbol(mpcq):
 
 
 def test_abi_version(mpcq):
-    assert mpcq.lib().mpcq_abi_version() == 2
+    assert mpcq.lib().mpcq_abi_version() == 3
 
 
 def test_default_params_match_reference(mpcq, golden16, oracle):

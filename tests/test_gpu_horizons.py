@@ -1,7 +1,8 @@
 """GPU parity at the fixture horizons besides 16 / 32 (test_gpu_parity.py): N = 4j <= 32,
-48, and round 3's N = 5, 6, 10, 13 (rows past N run as copies of stage N-1; odd N
+48, round 3's N = 5, 6, 10, 13 (rows past N run as copies of stage N-1; odd N
 makes the two sweep chains equally long), 33, 36, 40 (global workspace), 57 and 64
-(constraint values in the workspace too): formulation vs the reference fixtures,
+(constraint values in the workspace too), and round 4's 49 (13 waves) and 50 (the
+first horizon with the constraint values in the workspace): formulation vs the reference fixtures,
 the OSQP solve vs the oracle (statuses and iteration counts equal on every
 instance, x within X_TOL), the fused path on a synthetic batch, polish on the
 certified optimum x* (sessions: test_gpu_session.py).  The engine compiles every

@@ -194,6 +194,34 @@ def test_c5_size_launch(eng16, mpcq, oracle):
     assert np.abs(r["f0"][sel] - o["f0"]).max() < X_TOL
 
 
+def test_c4_full_size_launch_and_rank_shard(eng16, mpcq, oracle):
+    """BASELINE C4 at its real size on one GPU (65536 trot instances, bench.py's seed 2,
+    128 rounds of the grid): every instance solved; a strided sample of 512 equals the
+    oracle (status, iterations, forces within X_TOL).  Then rank 3's shard of the 8-GPU
+    split (8192 instances, generated alone as a rank does) launched by itself: bit for
+    bit the same rows as the whole launch."""
+    from mpcq import shard
+    total = 65536
+    b = shard.shard_batch(total, 1, 0, 16, ("trot",), seed=2)
+    r = eng16.solve(b["xref"], b["fsteps"], 0, want_x=False)
+    assert np.isin(r["status"], (1, 2)).all(), np.unique(r["status"], return_counts=True)
+    sel = np.arange(0, total, 128)
+    o = oracle.solve_batch(b["xref"][sel], b["fsteps"][sel], 0, nthreads=16)
+    assert np.array_equal(r["status"][sel], o["status"])
+    assert np.array_equal(r["iters"][sel], o["iters"])
+    err = np.abs(r["f0"][sel] - o["f0"]).max()
+    assert err < X_TOL
+    lo, hi = shard.shard_bounds(total, 8, 3)
+    s = shard.shard_batch(total, 8, 3, 16, ("trot",), seed=2)
+    assert np.array_equal(s["xref"], b["xref"][lo:hi]) and np.array_equal(s["fsteps"], b["fsteps"][lo:hi],
+                                                                             equal_nan=True)
+    rs = eng16.solve(s["xref"], s["fsteps"], 0, want_x=False)
+    for k in ("f0", "status", "iters"):
+        assert np.array_equal(rs[k], r[k][lo:hi], equal_nan=True), k
+    print(f"C4 65536: max|f0 - f0_oracle| on 512 {err:.2e}; iters median {np.median(r['iters'])} "
+          f"max {r['iters'].max()}; rank-3 shard of 8 bit-identical")
+
+
 def test_nonfinite_input(eng16, golden16, mpcq):
     Ax = golden16["Ax"][:2].copy()
     Ax[1, 100] = np.nan

@@ -358,6 +358,103 @@ __device__ __forceinline__ void schur_cols(double (&Ro)[12], const double (&G)[1
                                            const double (&c6)[6], std::integer_sequence<int, C...>) {
   (schur_col<C>(Ro, G, ca, c6), ...);
 }
+// i0 + sum_m c_m(lane J) g_m: twelve registers broadcast from one lane J of the row, the
+// broadcast folded into v_fmac_f64_dpp (as one asm block the compiler cannot hoist the
+// 144 broadcasts of a dense Schur update ahead of their products and spill them)
+#define MPCQ_BDOT_LANE(J)                                                                    \
+  asm("s_nop 1\n\t" \
+      "v_fmac_f64_dpp %0, %1, %13 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %2, %14 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %3, %15 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %4, %16 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %5, %17 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %6, %18 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %7, %19 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %8, %20 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %9, %21 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %10, %22 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %11, %23 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %12, %24 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" \
+      : "+v"(a0)                                                                             \
+      : "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]),   \
+        "v"(c[8]), "v"(c[9]), "v"(c[10]), "v"(c[11]), "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]),  \
+        "v"(g[4]), "v"(g[5]), "v"(g[6]), "v"(g[7]), "v"(g[8]), "v"(g[9]), "v"(g[10]), "v"(g[11]))
+template <int J>
+__device__ __forceinline__ double bdot_lane(const double (&c)[12], const double (&g)[12], double i0) {
+  double a0 = i0;
+  if constexpr (J == 0) MPCQ_BDOT_LANE(0);
+  else if constexpr (J == 1) MPCQ_BDOT_LANE(1);
+  else if constexpr (J == 2) MPCQ_BDOT_LANE(2);
+  else if constexpr (J == 4) MPCQ_BDOT_LANE(4);
+  else if constexpr (J == 5) MPCQ_BDOT_LANE(5);
+  else if constexpr (J == 6) MPCQ_BDOT_LANE(6);
+  else if constexpr (J == 8) MPCQ_BDOT_LANE(8);
+  else if constexpr (J == 9) MPCQ_BDOT_LANE(9);
+  else if constexpr (J == 10) MPCQ_BDOT_LANE(10);
+  else if constexpr (J == 12) MPCQ_BDOT_LANE(12);
+  else if constexpr (J == 13) MPCQ_BDOT_LANE(13);
+  else if constexpr (J == 14) MPCQ_BDOT_LANE(14);
+  else static_assert(J < 0, "a column lane LN(i)");
+  return a0;
+}
+#undef MPCQ_BDOT_LANE
+// The sparse Schur column of schur_col with its seven broadcasts folded into
+// v_fmac_f64_dpp (the cyclic reduction's factorisation runs two of these updates back
+// to back; as separate moves the compiler hoisted all 168 broadcasts and spilled them)
+#define MPCQ_BDOT7_LANE(J)                                                                   \
+  asm("s_nop 1\n\t" \
+      "v_fmac_f64_dpp %0, %1, %8 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %2, %9 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %3, %10 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %4, %11 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %5, %12 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %6, %13 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+      "v_fmac_f64_dpp %0, %7, %14 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" \
+      : "+v"(a0)                                                                             \
+      : "v"(ca), "v"(c6[0]), "v"(c6[1]), "v"(c6[2]), "v"(c6[3]), "v"(c6[4]), "v"(c6[5]), "v"(ga),  \
+        "v"(g6[0]), "v"(g6[1]), "v"(g6[2]), "v"(g6[3]), "v"(g6[4]), "v"(g6[5]))
+template <int J>
+__device__ __forceinline__ double bdot7_lane(double ca, const double (&c6)[6], double ga, const double (&g6)[6],
+                                             double i0) {
+  double a0 = i0;
+  if constexpr (J == 0) MPCQ_BDOT7_LANE(0);
+  else if constexpr (J == 1) MPCQ_BDOT7_LANE(1);
+  else if constexpr (J == 2) MPCQ_BDOT7_LANE(2);
+  else if constexpr (J == 4) MPCQ_BDOT7_LANE(4);
+  else if constexpr (J == 5) MPCQ_BDOT7_LANE(5);
+  else if constexpr (J == 6) MPCQ_BDOT7_LANE(6);
+  else if constexpr (J == 8) MPCQ_BDOT7_LANE(8);
+  else if constexpr (J == 9) MPCQ_BDOT7_LANE(9);
+  else if constexpr (J == 10) MPCQ_BDOT7_LANE(10);
+  else if constexpr (J == 12) MPCQ_BDOT7_LANE(12);
+  else if constexpr (J == 13) MPCQ_BDOT7_LANE(13);
+  else if constexpr (J == 14) MPCQ_BDOT7_LANE(14);
+  else static_assert(J < 0, "a column lane LN(i)");
+  return a0;
+}
+#undef MPCQ_BDOT7_LANE
+template <int CI>
+__device__ __forceinline__ void schur_col_a(double (&Ro)[12], const double (&G)[12], double ca,
+                                            const double (&c6)[6]) {
+  const double g6[6] = {G[6], G[7], G[8], G[9], G[10], G[11]};
+  Ro[CI] -= bdot7_lane<LN(CI)>(ca, c6, G[CI < 6 ? CI : CI - 6], g6, 0.0);
+}
+template <int... C>
+__device__ __forceinline__ void schur_cols_a(double (&Ro)[12], const double (&G)[12], double ca,
+                                             const double (&c6)[6], std::integer_sequence<int, C...>) {
+  (schur_col_a<C>(Ro, G, ca, c6), ...);
+}
+// Ro -= G C' for a dense 12x12 coupling C held one row per column lane (the reduced
+// system of the cyclic reduction): column CI takes row CI of C from lane LN(CI)
+template <int CI>
+__device__ __forceinline__ void schur_dcol(double (&Ro)[12], const double (&G)[12], const double (&C)[12]) {
+  Ro[CI] -= bdot_lane<LN(CI)>(C, G, 0.0);
+}
+template <int... C>
+__device__ __forceinline__ void schur_dcols(double (&Ro)[12], const double (&G)[12], const double (&Cm)[12],
+                                            std::integer_sequence<int, C...>) {
+  (schur_dcol<C>(Ro, G, Cm), ...);
+}
 
 // ---------------------------------------------------------------------------
 // Formulation pieces (restating MPC.py; oracle/mpcq_oracle.c is the CPU twin)
@@ -452,6 +549,49 @@ constexpr int kSlotPad = 2;
 template <int N>
 __host__ __device__ constexpr int SLOT(int q) { return GS * q + (q > N / 2 ? kSlotPad<N> : 0); }
 
+// One level of block cyclic reduction of the state system (round 4).  The odd
+// stages are eliminated stage-parallel: with T_{k,k-1} = L_k, T_{kk} = D_k,
+//   x_o = D_o^{-1} (b_o - L_o x_{o-1} - L_{o+1}' x_{o+1})        (o odd)
+// leaves a block-tridiagonal system on the even stages e = 2j (NS = N/2 of them)
+//   D'_j = D_e - L_e D_{e-1}^{-1} L_e' - L_{e+1}' D_{e+1}^{-1} L_{e+1}
+//   L''_j = -L_e D_{e-1}^{-1} L_{e-1}                              (T'_{j,j-1})
+//   b'_j = b_e - L_e D_{e-1}^{-1} b_{e-1} - L_{e+1}' D_{e+1}^{-1} b_{e+1}
+// which the two-ended sweep solves in N/2 + 1 dependent steps instead of N + 1:
+// per iteration the serial chain halves, for two stage-parallel phases (the
+// reduction of b and the back-substitution of the odd stages).
+// Measured and NOT the default (round 4, profiles/r04b_*, r04c_*): the factorisation
+// is faster (N = 16 87 k vs 103 k cycles, N = 32 109 k vs 144 k) and the sweep
+// shorter, but each of the two phases costs ~1450 cycles per iteration (~130
+// instructions per wave with four LDS round trips, plus a barrier) against ~200 per
+// sweep step saved: 1.81 -> 2.55 us per iteration alone at N = 16, 3.15 -> 4.09 at
+// N = 32; C2 126 k -> 88 k QP/s.  Lean phases would need the products L D^{-1}
+// precomputed per lane (24 doubles per lane), which neither LDS nor the VGPR budget
+// holds.  Build with -DMPCQ_CR to get it (parity-green on the GPU suite's CR horizons).
+#ifdef MPCQ_CR
+template <int N>
+constexpr bool kCR = N % 4 == 0 && N >= 8 && N <= 32;
+#else
+template <int N>
+constexpr bool kCR = false;
+#endif
+template <int N>
+struct CRL {  // offsets (doubles) of the reduction's arrays (kCR<N>)
+  static constexpr int NS = N / 2;
+  // in GH, past the reduced sweep's slots (SLOT<NS> reaches GS NS + 2): row i of
+  // D_o^{-1} of odd stage o at DI + GS (o >> 1) + RS i
+  static constexpr int DI = GS * NS + 2;
+  // in Sm, past the reduced S^{-1} slots: L_k compact, 48 doubles per stage: a[6]
+  // (L[i][i], i < 6), t[6] (L[i][6+i], i < 6), V[6][6] (L[6+i][6+j]); the other
+  // entries are structurally zero (Ctop)
+  static constexpr int LS = GS * NS + 2;
+  // in u.it.xs: the reduced sweep's states at SIGX<NS> slots (NS + 1 slots), then
+  // the odd stages' states, X of odd stage o at XO + 12 (o >> 1)
+  static constexpr int XO = 12 * (NS + 1);
+};
+static_assert(CRL<32>::DI + GS * 16 == GS * 32 + 2 && CRL<32>::LS + 48 * 32 <= GS * 32 + 2 &&
+                  CRL<32>::XO + 12 * 16 == 12 * 33,
+              "the reduction's arrays fit GH / Sm / xs");
+
 // Horizons beyond 32 stages do not fit a CU's LDS (N = 48: 236 KB): S^{-1}, F W and
 // R^{-1} Q move to a per-instance global workspace (LaunchArgs::work, work_doubles(N)
 // doubles per instance, L2-resident), the rest stays in LDS (N = 48: 140 KB).
@@ -516,6 +656,7 @@ struct Smem {
     } it;
     struct {
       double St[144], Sb[144];  // sweep hand-offs of the factorisation
+      double Lm[144];           // (kCR) the reduced meeting row's lower coupling
     } fa;
   } u;
   // per-wave partial reductions (32 per wave); during the sweeps the sink of lanes
@@ -557,7 +698,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
   if ((int64_t)blockIdx.x >= a.batch) return;
   const int64_t b = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;  // the instance
   STAMP_DECL
-  constexpr bool BIG = kBig<N>, ABG = kAbG<N>;
+  constexpr bool BIG = kBig<N>, ABG = kAbG<N>, CR = kCR<N>;
   // the scaled constraint values: LDS, or (N > 49) this instance's workspace (the
   // formulation-only launch builds them straight into its Ax output)
   using acd = std::conditional_t<ABG, const double, lds_cd>;
@@ -1097,6 +1238,178 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         }
         schur_cols(Ro, G, ca, c6, std::make_integer_sequence<int, 12>{});
       };
+      if constexpr (CR) {
+        // ---- cyclic reduction (kCR): D_o^{-1} of the odd stages, the reduced system
+        // on the even stages, then its two-ended factorisation (NS stages, dense
+        // couplings).  The stage-keyed scratch is dead once every lane holds its
+        // D / L rows (the barrier below); D^{-1} then reuses those GH slots.
+        constexpr int NS = CRL<N>::NS, MIDS = NS / 2;
+        const bool odd = (k & 1) != 0;
+        sync_all();
+        if (cl) {  // own row of L_k, compact (stage 0 has no L: zeros)
+          double* const q = &sh.Sm[0][0] + CRL<N>::LS + 48 * k;
+          if (ph < 6) {
+            q[ph] = k ? cta : 0.0;
+            q[6 + ph] = k ? ct6[ph] : 0.0;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) q[12 + 6 * (ph - 6) + j] = k ? ct6[j] : 0.0;
+          }
+        }
+        if (odd) {
+          double Ro[12];
+#pragma unroll
+          for (int ci = 0; ci < 12; ++ci) Ro[ci] = Dr0[ci];
+          gj12(Ro, ph, ok);
+          if (cl) {
+            double* const q = gh0 + CRL<N>::DI + GS * (k >> 1) + RS * ph;
+#pragma unroll
+            for (int ci = 0; ci < 12; ++ci) q[ci] = Ro[ci];
+          }
+        }
+        sync_all();
+        // Even stages: row ph of D'_j and of the reduced coupling the factorisation step of
+        // reduced stage j = k / 2 takes -- L''_j (lt: top rows and the meeting) or
+        // L''_{j+1}' (lb: bottom rows and the meeting) -- staged in LDS for the serial
+        // steps (held in registers across them they spilled): D' in GH slot SIG<NS>(j), the
+        // coupling row in Sm slot SIG<NS>(j) (each overwritten by its own row's G / S^{-1}
+        // at its step, after the read), the meeting row's lb past St / Sb in u.fa.
+        double* const lbm = sh.u.fa.Lm;  // the meeting row's lb (12 x 12)
+        // Ro -= (C S^{-1}) C' for the compact row (ca, c6) of a sparse coupling C; G = C S^{-1}
+        auto couple_sp = [&](double ca, const double (&c6)[6], const double* Sp, double (&Ro)[12],
+                             double (&G)[12]) __attribute__((always_inline)) {
+          const int ar = ph < 6 ? ph : ph - 6;
+#pragma unroll
+          for (int ci = 0; ci < 12; ++ci) {
+            double sv[7];
+            sv[0] = Sp[12 * ar + ci];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) sv[1 + j] = Sp[12 * (6 + j) + ci];
+            double gv = ca * sv[0];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) gv = fma(c6[j], sv[1 + j], gv);
+            G[ci] = gv;
+            asm volatile("" ::: "memory");
+          }
+          schur_cols_a(Ro, G, ca, c6, std::make_integer_sequence<int, 12>{});
+        };
+        if (!odd) {
+          const int jr = k >> 1;
+          const double* const Lsb = &sh.Sm[0][0] + CRL<N>::LS;
+          double* const lslot = &sh.Sm[0][0] + SLOT<NS>(SIG<NS>(jr)) + RS * ph;
+          double Dp[12], G[12];
+#pragma unroll
+          for (int ci = 0; ci < 12; ++ci) Dp[ci] = Dr0[ci];
+          if (k >= 1) {  // - L_k D_{k-1}^{-1} L_k'
+            couple_sp(cta, ct6, gh0 + CRL<N>::DI + GS * ((k - 1) >> 1), Dp, G);
+            if (k >= 2 && jr <= MIDS) {  // lt = -(L_k D_{k-1}^{-1}) L_{k-1}, row ph
+              const double* const q = Lsb + 48 * (k - 1);
+              double lt[12];
+#pragma unroll
+              for (int c_ = 0; c_ < 6; ++c_) lt[c_] = -(G[c_] * q[c_]);
+#pragma unroll
+              for (int jj = 0; jj < 6; ++jj) {
+                double v = G[jj] * q[6 + jj];
+#pragma unroll
+                for (int m_ = 0; m_ < 6; ++m_) v = fma(G[6 + m_], q[12 + 6 * m_ + jj], v);
+                lt[6 + jj] = -v;
+              }
+              if (cl) {
+#pragma unroll
+                for (int ci = 0; ci < 12; ++ci) lslot[ci] = lt[ci];
+              }
+            }
+          }
+          // - L_{k+1}' D_{k+1}^{-1} L_{k+1} (k + 1 <= N - 1: N is even)
+          couple_sp(cba, cb6, gh0 + CRL<N>::DI + GS * (k >> 1), Dp, G);
+          if (k + 2 <= N - 1 && jr >= MIDS) {  // lb = -(L_{k+1}' D_{k+1}^{-1}) L_{k+2}', row ph
+            const double* const q = Lsb + 48 * (k + 2);
+            double lb[12];
+#pragma unroll
+            for (int c_ = 0; c_ < 6; ++c_) lb[c_] = -(G[c_] * q[c_] + G[6 + c_] * q[6 + c_]);
+#pragma unroll
+            for (int jj = 0; jj < 6; ++jj) {
+              double v = G[6] * q[12 + 6 * jj];
+#pragma unroll
+              for (int m_ = 1; m_ < 6; ++m_) v = fma(G[6 + m_], q[12 + 6 * jj + m_], v);
+              lb[6 + jj] = -v;
+            }
+            if (cl) {
+              double* const d = jr == MIDS ? lbm + 12 * ph : lslot;
+#pragma unroll
+              for (int ci = 0; ci < 12; ++ci) d[ci] = lb[ci];
+            }
+          }
+          if (cl) {
+            double* const d = gh0 + SLOT<NS>(SIG<NS>(jr)) + RS * ph;
+#pragma unroll
+            for (int ci = 0; ci < 12; ++ci) d[ci] = Dp[ci];
+          }
+        }
+        sync_all();
+        // one coupling of the reduced factorisation: Ro -= (C S^{-1}) C' for the dense
+        // row C of this lane, S^{-1} (St / Sb) row by row; -G stored at Gd
+        auto couple_dn = [&](const double (&C)[12], const double* Sp, double* Gd, double (&Ro)[12])
+            __attribute__((always_inline)) {
+          double G[12];
+#pragma unroll
+          for (int ci = 0; ci < 12; ++ci) G[ci] = 0.0;
+#pragma unroll
+          for (int m_ = 0; m_ < 12; ++m_) {
+            double sr[12];
+#pragma unroll
+            for (int ci = 0; ci < 12; ++ci) sr[ci] = Sp[12 * m_ + ci];
+#pragma unroll
+            for (int ci = 0; ci < 12; ++ci) G[ci] = fma(C[m_], sr[ci], G[ci]);
+            asm volatile("" ::: "memory");
+          }
+          wave_sync();  // the row's reads of the slot G goes to are done
+          if (cl) {
+#pragma unroll
+            for (int ci = 0; ci < 12; ++ci) Gd[ci] = -G[ci];
+          }
+          schur_dcols(Ro, G, C, std::make_integer_sequence<int, 12>{});
+        };
+        // the reduced system's two-ended factorisation (as below, on NS stages): step
+        // jj < MIDS: top reduced stage jj and bottom NS-1-jj > MIDS; step MIDS: the meeting
+#pragma nounroll
+        for (int jj = 0; jj <= MIDS; ++jj) {
+          launder();
+          const int j = k >> 1;
+          const bool ev = (k & 1) == 0, mid = jj == MIDS;
+          const bool top = ev && !mid && j == jj, bot = ev && !mid && j == NS - 1 - jj && j > MIDS,
+                     mrow = ev && mid && j == MIDS;
+          if (top || bot || mrow) {
+            const bool useT = (top && j > 0) || mrow, useB = (bot && j < NS - 1) || mrow;
+            double* const gs = gh0 + SLOT<NS>(SIG<NS>(j)) + RS * ph;
+            const double* const ls = &sh.Sm[0][0] + SLOT<NS>(SIG<NS>(j)) + RS * ph;
+            double Ro[12], C[12];
+#pragma unroll
+            for (int ci = 0; ci < 12; ++ci) { Ro[ci] = gs[ci]; C[ci] = ls[ci]; }
+            if (useT) couple_dn(C, St, gs, Ro);
+            if (useB) {
+              if (mrow) {
+#pragma unroll
+                for (int ci = 0; ci < 12; ++ci) C[ci] = lbm[12 * ph + ci];
+              }
+              couple_dn(C, Sb, gh0 + SLOT<NS>(SIG<NS>(j + 1)) + RS * ph, Ro);
+            }
+            gj12(Ro, ph, ok);
+            wave_sync();  // the row's reads of its coupling slot are done
+            if (cl) {
+#pragma unroll
+              for (int ci = 0; ci < 12; ++ci) SmW[SLOT<NS>(SIG<NS>(j)) + RS * ph + ci] = Ro[ci];
+            }
+            wave_sync();  // the previous inverse has been consumed by this row
+            if (cl) {
+              double* dst = mrow ? &sh.GH[0][RS * ph] : (bot ? Sb : St) + 12 * ph;
+#pragma unroll
+              for (int ci = 0; ci < 12; ++ci) dst[ci] = Ro[ci];
+            }
+          }
+          sync_all();
+        }
+      } else {
       // Step j < MID: top row k = j and bottom row k = N-1-j > MID in parallel; step
       // MID: the meeting row (both couplings).  M^{-1} -> GH[0].
 #pragma nounroll
@@ -1125,6 +1438,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         }
         sync_all();
       }
+      }  // !CR
       STAMP(14);
       // a non-positive pivot anywhere fails the whole instance (uniform result)
       if (!ok) atomicOr(&sh.flag[2], 1);
@@ -1181,9 +1495,15 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       o.oXSp = 12 * k + ph;  // natural order (update_info)
       o.oXSp6 = 12 * k + (ph < 6 ? ph + 6 : ph);
       // the sweep's states in its slots (SIGX): own X_{k+1}, the previous stage's X_k
-      o.rXS = 12 * SIGX<N>(k + 1) + ph;
-      o.rXSpm = hp_ ? 12 * SIGX<N>(k) + ph : zXS;
-      o.rXSp6m = hp_ ? 12 * SIGX<N>(k) + (ph < 6 ? ph + 6 : ph) : zXS;
+      // (cyclic reduction: the even stages' states in the reduced sweep's slots, the
+      // odd ones after them)
+      auto xsl = [](int kk) __attribute__((always_inline)) -> int {
+        if constexpr (kCR<N>) return (kk & 1) ? CRL<N>::XO + 12 * (kk >> 1) : 12 * SIGX<CRL<N>::NS>((kk >> 1) + 1);
+        else return 12 * SIGX<N>(kk + 1);
+      };
+      o.rXS = xsl(k) + ph;
+      o.rXSpm = hp_ ? xsl(k - 1) + ph : zXS;
+      o.rXSp6m = hp_ ? xsl(k - 1) + (ph < 6 ? ph + 6 : ph) : zXS;
       o.oHdm = hp_ ? o.oHd : zAb;
       o.oH6m = hp_ && !isv_ ? o.oH6 : zAb;
       o.oFWcm = isv_ ? oFWc : zFW;
@@ -2055,7 +2375,13 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           wave_sync();
           }  // MPCQ_REP_SWEEP
       };
-      auto ph_sweep_lag = [&]() __attribute__((always_inline)) {
+      // NS: stages of the system swept (N, or N / 2 after the cyclic reduction); RB: its
+      // right-hand side (RB[q] + RB[q + RO]), YVB: its y / w slots, XSB: its states
+      // (ST: the stamp bucket of the wait for the right-hand sides, diagnostic builds)
+      auto ph_sweep_lag = [&](auto ns_tag, auto st_tag, lds_cd* const RB, int RO, double* const YVB,
+                              double* const XSB) __attribute__((always_inline)) {
+          constexpr int NS = decltype(ns_tag)::value, MID = NS / 2, BOT = NS - 1 - MID;
+          [[maybe_unused]] constexpr int ST = decltype(st_tag)::value;
           // P5-P7: the state solve on wave 0 alone (no block barrier inside), up to 32
           // stages (beyond: ph_sweep_split).
           // Inward step j = 1..MID: top kk(j) = j, bottom kk(j) = N-1-j.  Half 0 (rows
@@ -2083,8 +2409,8 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           using swp2 = lds_cd2;
           swp* const GHs = GHr;
           // (the bottom chain's slots are past N/2: +2, SLOT)
-          swp* const Mb = half == 0 ? GHs + (GS * (cr == 0 ? 0 : MID) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_)
-                                    : (lds_cd*)&sh.Sm[0][0] + (GS * (cr == 0 ? -2 : MID - 1) + (cr == 0 ? 0 : kSlotPad<N>) + RS * rr_);
+          swp* const Mb = half == 0 ? GHs + (GS * (cr == 0 ? 0 : MID) + (cr == 0 ? 0 : kSlotPad<NS>) + RS * rr_)
+                                    : (lds_cd*)&sh.Sm[0][0] + (GS * (cr == 0 ? -2 : MID - 1) + (cr == 0 ? 0 : kSlotPad<NS>) + RS * rr_);
           double g[12];
           auto row12 = [&](swp* q) __attribute__((always_inline)) {  // 16-B aligned row: 6 ds_read_b128
 #pragma unroll
@@ -2106,11 +2432,11 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           };
           if (t < 64) row12(rowp(1));
           sync_all();
-          STAMP(3);
+          STAMP(ST);
           // outward step j reads G_{MID-j+1}' (top, slot MID+1-j) / H_{MID+j-1}'
           // (bottom, slot N-j) columns: Ob + (MID - j) GS (LDS offsets are unsigned,
           // so the bases sit at the lowest slot a chain reaches)
-          lds_cd* const Ob = GHr + (GS * (cr == 0 ? 1 : N - MID) + (cr == 0 ? 0 : kSlotPad<N>) + rr_);
+          lds_cd* const Ob = GHr + (GS * (cr == 0 ? 1 : NS - MID) + (cr == 0 ? 0 : kSlotPad<NS>) + rr_);
           if (t < 64) {
             // the sweeps are every wave's critical path (the other waves of the
             // instance wait at the barrier): issue them ahead of a co-resident
@@ -2119,15 +2445,15 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             // right-hand side of step j: top stage j (slot j), bottom stage N-1-j (slot
             // MID+1+j, except the meeting stage MID at the bottom's last step BOT, slot
             // MID, which the bottom re-reads in the steps it does not take); na at +12N
-            lds_cd* const Bb = (lds_cd*)&sh.u.it.bo[0][0] + (12 * (cr == 0 ? 0 : MID + 1) + rr_);
-            lds_cd* const Bm = (lds_cd*)&sh.u.it.bo[MID][rr_];
+            lds_cd* const Bb = RB + (12 * (cr == 0 ? 0 : MID + 1) + rr_);
+            lds_cd* const Bm = RB + (12 * MID + rr_);
             auto rhs = [&](int j) __attribute__((always_inline)) -> lds_cd* {  // j: a constant
               return (j >= BOT && cr != 0) ? Bm : Bb + 12 * j;
             };
             // w of stage kk(j-2) (half 1): top slot j-2, bottom slot MID-1+j; the other
             // lanes store into the sink with the same stride
             lds_d* const sink = (lds_d*)&sh.red[0] + (t & 31);
-            lds_d* const Yb = (half == 1 && s < 12) ? (lds_d*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? -2 : MID - 1) + rr_)
+            lds_d* const Yb = (half == 1 && s < 12) ? (lds_d*)YVB + (12 * (cr == 0 ? -2 : MID - 1) + rr_)
                                                     : sink;
             // right-hand sides run two steps ahead: step j sums the one of step j+1
             // (loaded during step j-1) and loads the one of step j+2; half 1 (the w
@@ -2135,12 +2461,12 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             // are loaded together and waited for once: they were published by the
             // barrier just passed, so this round trip is on the critical path.
             const double m0 = half == 0 ? 1.0 : 0.0;
-            double s0 = rhs(0)[0], s1 = rhs(0)[12 * N];
-            double c0 = rhs(1)[0], c1 = rhs(1)[12 * N];
+            double s0 = rhs(0)[0], s1 = rhs(0)[RO];
+            double c0 = rhs(1)[0], c1 = rhs(1)[RO];
             asm volatile("" : "+v"(s0), "+v"(s1), "+v"(c0), "+v"(c1));
             double src = half == 0 ? s0 + s1 : 0.0;  // y_kk(0) (half 0)
             double bcn = (c0 + c1) * m0;
-            double b0 = rhs(2)[0], b1 = rhs(2)[12 * N];
+            double b0 = rhs(2)[0], b1 = rhs(2)[RO];
 #pragma unroll
             for (int j = 1; j <= MID + 1; ++j) {
               asm volatile("" : : : "memory");
@@ -2152,8 +2478,8 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
                 row12(rowp(j + 1));
               } else if (j == MID) {  // the meeting step: M^{-1} rows (half 0), the S walk (half 1)
                 row12(half == 0 ? GHs + RS * rr_ : rowp(MID + 1));
-                lds_cd* qb = (lds_cd*)&sh.u.it.bo[MID][rr_];
-                b0 = qb[0]; b1 = qb[12 * N];
+                lds_cd* qb = RB + (12 * MID + rr_);
+                b0 = qb[0]; b1 = qb[RO];
               } else {  // the last step: the first outward step's columns
 #pragma unroll
                 for (int i = 0; i < 12; ++i) g[i] = Ob[RS * i + GS * (MID - 1)];
@@ -2168,12 +2494,12 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               asm volatile("" : "+v"(b0), "+v"(b1));
               if (j < MID) bcn = (b0 + b1) * m0;
               if (j + 2 <= MID) {
-                b0 = rhs(j + 2)[0]; b1 = rhs(j + 2)[12 * N];
+                b0 = rhs(j + 2)[0]; b1 = rhs(j + 2)[RO];
               }
               if (j >= 2 && j <= MID) {  // half 1: w of stage kk(j-2)
                 Yb[12 * j] = acc;
               } else if (j == MID + 1) {  // even N: the bottom's kk(MID-1) is the meeting stage (no w)
-                if constexpr (N & 1) Yb[12 * j] = acc;
+                if constexpr (NS & 1) Yb[12 * j] = acc;
                 else *(cr == 0 ? Yb + 12 * j : sink) = acc;
               }
               if (j <= MID) {
@@ -2183,7 +2509,11 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
                 src = keep_lo_take_lo(adv ? acc : src, src);
               } else {
                 xp = acc;
-                if (cr == 0 && half == 0 && s < 12) sh.u.it.xs[SIGX<N>(MID + 1)][rr_] = xp;
+                // (lane ids from a laundered thread index: held across the loop, the
+                // condition's operand was spilled and its reload waited for here)
+                int tl_ = t;
+                asm volatile("" : "+v"(tl_));
+                if (((tl_ >> 4) & 3) == 0 && (tl_ & 15) < 12) XSB[12 * SIGX<NS>(MID + 1) + (tl_ & 15)] = xp;
               }
             }
             STAMP(6);
@@ -2196,9 +2526,9 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             // top slot MID+1-j, bottom slot N-j (SIGX; Xb - 12 j).  The bottom row's last
             // step (kk = N) is idle: its store goes to the sink.
             // (bases at step MID's slot: step j at base + 12 (MID - j))
-            lds_cd* const Wb = (lds_cd*)&sh.u.it.yv[0][0] + (12 * (cr == 0 ? 0 : N - MID) + rr_);
+            lds_cd* const Wb = (lds_cd*)YVB + (12 * (cr == 0 ? 0 : NS - MID) + rr_);
             lds_d* const sinkO = (lds_d*)&sh.red[0] + (t & 31);
-            lds_d* const Xb = (half == 0 && s < 12) ? (lds_d*)&sh.u.it.xs[0][0] + (12 * (cr == 0 ? 1 : N - MID) + rr_)
+            lds_d* const Xb = (half == 0 && s < 12) ? (lds_d*)XSB + (12 * (cr == 0 ? 1 : NS - MID) + rr_)
                                                     : sinkO;
             wave_sync();  // the w written by half 1
             double bq = Wb[12 * (MID - 1)];
@@ -2221,7 +2551,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               if (j < MID) {
                 xp = acc;
                 Xb[12 * (MID - j)] = acc;
-              } else if constexpr (N & 1) {
+              } else if constexpr (NS & 1) {
                 *Xb = acc;
               } else {  // even N: the bottom chain has no step MID
                 *(cr == 0 ? Xb : sinkO) = acc;
@@ -2232,10 +2562,126 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           wave_sync();
           }  // MPCQ_REP_SWEEP
       };
-      // the state sweep: the lagging form up to 32 stages, the split form beyond
+      // ---- the cyclic reduction's stage-parallel phases (kCR) ------------------
+      // L_kk on the compact store, per lane: (L v)[ph] = cA v[ph] + cT v[ph +- 6] +
+      // sum_j cV[j] v[6 + j], v(lane LN(i)) = v[i]; the structural zeros read sh.zero.
+      // Row ph of L_kk:
+      auto cr_lrow = [&](int kk, double& cA, double& cT, double (&cV)[6]) __attribute__((always_inline)) {
+        lds_cd* const q = (lds_cd*)&sh.Sm[0][0] + CRL<N>::LS + 48 * kk;
+        lds_cd* const zz = (lds_cd*)sh.zero;
+        const bool lo = ph < 6;
+        cA = *(lo ? q + ph : zz);
+        cT = *(lo ? q + 6 + ph : zz);
+        lds_cd* const qv = lo ? zz : q + 12 + 6 * (ph - 6);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) cV[j] = qv[j];
+      };
+      // column ph of L_kk (a row of L_kk')
+      auto cr_lcol = [&](int kk, double& cA, double& cT, double (&cV)[6]) __attribute__((always_inline)) {
+        lds_cd* const q = (lds_cd*)&sh.Sm[0][0] + CRL<N>::LS + 48 * kk;
+        lds_cd* const zz = (lds_cd*)sh.zero;
+        const bool lo = ph < 6;
+        cA = *(lo ? q + ph : zz);
+        cT = *(lo ? zz : q + ph);  // t[ph - 6] at q + 6 + (ph - 6)
+        lds_cd* const qv = lo ? zz : q + 12 + (ph - 6);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) cV[j] = qv[6 * j];
+      };
+      auto cr_apply = [&](double cA, double cT, const double (&cV)[6], double v) __attribute__((always_inline)) {
+        const double vr = dppd<0x128>(v);  // row_ror:8: component ph +- 6 (LN(j + 6) = LN(j) + 8)
+        return bdot_ln6v(cV, v, fma(cT, vr, cA * v));
+      };
+      // P_ab: the reduced right-hand side.  Lanes of even stage k form
+      //   b'_{k/2} = b_k - L_k u_a - L_{k+1}' u_b,  u_a = D_{k-1}^{-1} b_{k-1} (this row),
+      //   u_b = D_{k+1}^{-1} b_{k+1} (the odd row below, its own product, handed up by
+      // permlane16), split over the two halves the sweep sums (RB[q], RB[q + 12 NS]).
+      // Branch-free: every lane computes, the odd rows' stores go to the sink.
+      auto cr_reduce = [&]() __attribute__((always_inline)) {
+        constexpr int NS = CRL<N>::NS;
+        launder();
+        const bool ev = (k & 1) == 0;
+        lds_cd* const BO = (lds_cd*)&sh.u.it.bo[0][0];  // b = bo + na (na at + 12 N)
+        const int kb = ev ? (k >= 1 ? k - 1 : 0) : k;
+        const int sb = 12 * SIG<N>(kb) + ph;
+        const double bv = BO[sb] + BO[sb + 12 * N];
+        const int di = (ev ? (k >= 1 ? k - 1 : 0) : k) >> 1;
+        lds_cd* const Mr = (ev && k == 0) ? (lds_cd*)sh.zero : GHr + (CRL<N>::DI + GS * di + RS * ph);
+        double g[12];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const dbl2 v = ((lds_cd2*)Mr)[i];
+          g[2 * i] = v.x;
+          g[2 * i + 1] = v.y;
+        }
+        const double so_b = BO[12 * SIG<N>(k) + ph], so_n = BO[12 * SIG<N>(k) + ph + 12 * N];
+        double cA, cT, cV[6], dA, dT, dV[6];
+        cr_lrow(k, cA, cT, cV);
+        cr_lcol(k + 1 <= N - 1 ? k + 1 : N - 1, dA, dT, dV);
+        const double u = bdot_ln12(g, bv, 0.0);  // row ph of D^{-1} b (lane LN(i) holds b[i])
+        double ub;
+        {  // rows 0 <- 1, 2 <- 3: the odd row's u (permlane16_swap's second result)
+          const long long bb = __double_as_longlong(u);
+          const auto lo_ = __builtin_amdgcn_permlane16_swap((unsigned)bb, (unsigned)bb, false, false);
+          const auto hi_ = __builtin_amdgcn_permlane16_swap((unsigned)(bb >> 32), (unsigned)(bb >> 32), false, false);
+          ub = __longlong_as_double(((long long)hi_[1] << 32) | lo_[1]);
+        }
+        const double la = cr_apply(cA, cT, cV, u);
+        const double lb_ = cr_apply(dA, dT, dV, ub);
+        double* const W1 = &sh.u.it.nb[0][0] + (12 * SIG<NS>(k >> 1) + ph);
+        const bool st = cl && ev;
+        *(st ? W1 : Wdump) = (so_b + so_n) - la;
+        *(st ? W1 + 12 * NS : Wdump) = -lb_;
+      };
+      // P_c: the odd stages' states, x_k = D_k^{-1} (b_k - L_k x_{k-1} - L_{k+1}' x_{k+1})
+      // from the reduced sweep's even states; stored after the reduced states (CRL::XO)
+      auto cr_back = [&]() __attribute__((always_inline)) {
+        constexpr int NS = CRL<N>::NS;
+        launder();
+        const bool od = (k & 1) != 0;
+        lds_cd* const XS = (lds_cd*)&sh.u.it.xs[0][0];
+        lds_cd* const BO = (lds_cd*)&sh.u.it.bo[0][0];
+        const bool hn = k + 1 <= N - 1;
+        const double xm = XS[12 * SIGX<NS>(((k >= 1 ? k - 1 : 0) >> 1) + 1) + ph];
+        const double xp = *(hn ? XS + (12 * SIGX<NS>(((k + 1) >> 1) + 1) + ph) : (lds_cd*)sh.zero);
+        double cA, cT, cV[6], dA, dT, dV[6];
+        cr_lrow(k, cA, cT, cV);
+        cr_lcol(hn ? k + 1 : N - 1, dA, dT, dV);
+        lds_cd* const Mr = GHr + (CRL<N>::DI + GS * (k >> 1) + RS * ph);
+        double g[12];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const dbl2 v = ((lds_cd2*)Mr)[i];
+          g[2 * i] = v.x;
+          g[2 * i + 1] = v.y;
+        }
+        const int so = 12 * SIG<N>(k) + ph;
+        const double bk = BO[so] + BO[so + 12 * N];
+        const double r = (bk - cr_apply(cA, cT, cV, xm)) - cr_apply(dA, dT, dV, xp);
+        const double x = bdot_ln12(g, r, 0.0);
+        double* const Xo = &sh.u.it.xs[0][0] + (CRL<N>::XO + 12 * (k >> 1) + ph);
+        *((cl && od) ? Xo : Wdump) = x;
+      };
+      // the state sweep: the lagging form up to 32 stages (on the reduced system when
+      // kCR), the split form beyond
       auto ph_sweep = [&]() __attribute__((always_inline)) {
-        if constexpr (BIG) ph_sweep_split();
-        else ph_sweep_lag();
+        if constexpr (BIG) {
+          ph_sweep_split();
+        } else if constexpr (CR) {
+          constexpr int NS = CRL<N>::NS;
+          sync_all();  // ph_rhs's right-hand sides
+          STAMP(3);
+          cr_reduce();
+          // (its barrier publishes the reduced right-hand sides)
+          ph_sweep_lag(std::integral_constant<int, NS>{}, std::integral_constant<int, 15>{},
+                       (lds_cd*)&sh.u.it.nb[0][0], 12 * NS, &sh.u.it.yv[0][0], &sh.u.it.xs[0][0]);
+          sync_all();  // the even stages' states
+          STAMP(12);   // (diagnostic builds: the outward sweep and this barrier)
+          cr_back();
+          // (ph_recover's barrier publishes the odd stages' states)
+        } else {
+          ph_sweep_lag(std::integral_constant<int, N>{}, std::integral_constant<int, 3>{},
+                       (lds_cd*)&sh.u.it.bo[0][0], 12 * N, &sh.u.it.yv[0][0], &sh.u.it.xs[0][0]);
+        }
       };
       // ri0: 1/rho of the own slot-0 row (the ADMM loop's, or polish's)
       auto ph_recover = [&](const RhsOps* op, double ri0, double uf, double beta, double& sf, double& sX,

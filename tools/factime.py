@@ -2,8 +2,9 @@
 import os, sys, numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpc-tsid_amd"))
 import mpcq
-eng = mpcq.Engine(16)
-src = mpcq.synth.make_batch(1024, 16, gaits=("trot",), seed=2)
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+eng = mpcq.Engine(N)
+src = mpcq.synth.make_batch(1024, N, gaits=("trot",), seed=2)
 info = np.empty((1024, 4), np.int32)
 import ctypes as C
 from mpcq import _lib as L

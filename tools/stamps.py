@@ -15,12 +15,20 @@ os.environ.setdefault("MPCQ_LIB_VARIANT", "stamps")
 
 NAMES = ["prologue", "scaling", "factor", "iter:w,b,u,beta,bt", "chk:publish", "chk:primal", "iter:inward sweeps+S^-1 y",
          "iter:outward sweeps", "chk:dual", "iter:forces", "iter:z/y/x update", "chk:reduce+adapt", "epilogue", "fac:phaseP", "fac:phaseS"]
+# the cyclic-reduction build (kCR horizons): bucket 3 is ph_rhs + its barrier, 15 the
+# reduction of b + its barrier, 12 the outward sweep + the barrier after it, 7 the
+# back-substitution of the odd stages + ph_recover's barrier
+NAMES_CR = list(NAMES) + ["cr:reduce b + barrier"]
+NAMES_CR[3] = "iter:w,b,u,beta + barrier"
+NAMES_CR[7] = "cr:odd stages + barrier"
+NAMES_CR[12] = "iter:outward + barrier (+epilogue)"
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--N", type=int, default=16)
+    ap.add_argument("--cr", action="store_true", help="label the buckets of the cyclic-reduction build")
     ap.add_argument("--copies", type=int, default=-1,
                     help=">= 0: every instance a copy of this instance of the C2 batch (seed 2)")
     a = ap.parse_args()
@@ -45,11 +53,12 @@ def main():
     torch.cuda.synchronize()
     S = stamps.cpu().numpy().astype(np.float64)
     its = it.cpu().numpy()
-    tot = S[:, :13].sum(axis=1)
+    names = NAMES_CR if a.cr else NAMES
+    tot = S[:, :13].sum(axis=1) + (S[:, 15] if a.cr else 0.0)
     print(f"batch {a.batch} N={a.N}: iters median {np.median(its)} max {its.max()}; "
           f"kernel ms (event) {eng.last_kernel_ms()[1]:.2f}")
     print(f"cycles per instance: median {np.median(tot):.3e}; per iteration {np.median(tot / its):.0f}")
-    for i, nm in enumerate(NAMES):
+    for i, nm in enumerate(names):
         share = S[:, i] / tot
         per_it = S[:, i] / its
         print(f"  {nm:18s} share {np.median(share) * 100:6.2f}%   cycles/iter {np.median(per_it):9.0f}")

@@ -574,6 +574,23 @@ constexpr bool kCR = N % 4 == 0 && N >= 8 && N <= 32;
 template <int N>
 constexpr bool kCR = false;
 #endif
+// The deferred termination check (round 4).  A check that is not an adaptive-rho
+// step and not the last iteration runs inside the next iteration ("the carrier"): the
+// checked iteration publishes its states / duals and the cheap infeasibility partials
+// (no barrier), the carrier's own right-hand-side barrier publishes them, every wave
+// but the sweep wave forms its stages' residual terms while wave 0 runs the sweep
+// (wave 0 after it), and after the force-recovery barrier every lane combines them:
+// a converged (or infeasible) check stops the solve before the carrier's z / y / x
+// update, so the result is the checked iteration's -- the same decisions, iteration
+// counts and bits as the blocking check, which stays for the adaptive-rho steps, the
+// last iteration and beyond 32 stages.
+#ifdef MPCQ_NO_DC
+template <int N>
+constexpr bool kDC = false;  // (A/B builds: every check blocking)
+#else
+template <int N>
+constexpr bool kDC = N <= 32 && !kCR<N>;
+#endif
 template <int N>
 struct CRL {  // offsets (doubles) of the reduction's arrays (kCR<N>)
   static constexpr int NS = N / 2;
@@ -663,6 +680,10 @@ struct Smem {
   // whose store is void (lane (t & 31) + 12 j, j <= N/2 + 1)
   double red[(8 * kRows<N> + 32 > 12 * (N / 2 + 2) + 32) ? 8 * kRows<N> + 32 : 12 * (N / 2 + 2) + 32];
   double dump[64];          // sink of predicated stores (never read): lane & 63
+  // (kDC) the deferred check: the checked iteration's states X_{k+1} (the duals go to
+  // u.it.nb), and per wave 16 residual maxima + the cheap infeasibility partials
+  double ckx[kDC<N> ? N : 1][12];
+  double dcp[kDC<N> ? 24 * (kRows<N> / 4) : 1];
   alignas(16) double zero[72];  // zeros: masked coefficient reads point here instead of selecting
   int flag[4];
 };
@@ -1734,9 +1755,12 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       asm volatile("" : "+v"(epi0), "+v"(edi0));
     };
     double dyp[3];     // delta_y projected onto the polar of the recession cone of [l, u]
-    // cv: the constant block, read by the caller ahead of the check (ck_all)
-    auto infeas_cheap = [&](const double (&dy)[3], double dxf, double dxX, const double (&cv)[CK_COUNT])
-        __attribute__((always_inline)) {
+    // The cheap part of OSQP's infeasibility tests on the last iteration's deltas, own
+    // data only: dyp, and this wave's maxima ||E dy|| / ||D dx|| / ||D^-1 P dx|| and sum
+    // u'dy+ + l'dy- into P[PS wv + 16 + {0, 2, 3, 6}] (red for the blocking check, dcp
+    // for the deferred one).  cv: the constant block, read ahead of the check (ck_all).
+    auto cheap_partials = [&](const double (&dy)[3], double dxf, double dxX, const double (&cv)[CK_COUNT],
+                              double* const P, int PS) __attribute__((always_inline)) {
       MPCQ_CHECK_IDS();
       double lob[3], hib[3];
       chk_bounds(cv, lob, hib);
@@ -1744,13 +1768,6 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       for (int j = 0; j < 3; ++j) {
         const bool uinf = hib[j] > kInf * kMinScaling, linf = lob[j] < -kInf * kMinScaling;
         dyp[j] = uinf ? (linf ? 0.0 : fmin(dy[j], 0.0)) : (linf ? fmax(dy[j], 0.0) : dy[j]);
-      }
-      // published together with update_info's states / duals, one barrier for both
-      if (cl) {
-        sh.u.it.na[k][ph] = dxX;
-        sh.u.it.nb[k][ph] = dyp[0];
-        sh.u.it.yv[k][ph] = xX;
-        sh.u.it.bo[k][ph] = y[0];
       }
       double ndy = 0.0, ineq = 0.0;
 #pragma unroll
@@ -1784,8 +1801,19 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         ineq = __longlong_as_double(((long long)hi_[0] << 32) | lo_[0]) +
                __longlong_as_double(((long long)hi_[1] << 32) | lo_[1]);
       }
-      if (lane == 0 || lane == 4 || lane == 8) sh.red[32 * wv + 16 + (lane == 0 ? 0 : 2 + (lane >> 3))] = mine;
-      if (lane == 6) sh.red[32 * wv + 16 + 6] = ineq;
+      if (lane == 0 || lane == 4 || lane == 8) P[PS * wv + 16 + (lane == 0 ? 0 : 2 + (lane >> 3))] = mine;
+      if (lane == 6) P[PS * wv + 16 + 6] = ineq;
+    };
+    auto infeas_cheap = [&](const double (&dy)[3], double dxf, double dxX, const double (&cv)[CK_COUNT])
+        __attribute__((always_inline)) {
+      cheap_partials(dy, dxf, dxX, cv, sh.red, 32);
+      // published together with update_info's states / duals, one barrier for both
+      if (cl) {
+        sh.u.it.na[k][ph] = dxX;
+        sh.u.it.nb[k][ph] = dyp[0];
+        sh.u.it.yv[k][ph] = xX;
+        sh.u.it.bo[k][ph] = y[0];
+      }
       sync_all();  // (update_info(INF) relies on this barrier for its own publication)
     };
     // the products, where a cheap condition holds (inf_need != 0, uniform): A' dy for
@@ -1841,24 +1869,18 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     // of each row then owns residual quantity s, reduced over the wave's rows by
     // permlane swaps and over the waves through red[].  INF: also combine the
     // cheap partials of infeas_cheap into inf_need.
-    // INF: after infeas_cheap, which has published the states / duals with its deltas
-    auto update_info = [&](auto inf_tag, const double (&cv)[CK_COUNT]) __attribute__((always_inline)) {
-      constexpr bool INF = decltype(inf_tag)::value;
+    // info_terms: this wave's 16 residual maxima into D[DS wv + 0..15], from the own
+    // rows / columns and the published states XP (X_{k'} of stage k' at 12 (k' - 1))
+    // and duals WD (y of stage k' at 12 k')
+    auto info_terms = [&](const double (&cv)[CK_COUNT], lds_cd* const XP, const double* WD, double* const D,
+                          int DS) __attribute__((always_inline)) {
       MPCQ_CHECK_IDS();
-      if constexpr (!INF) {
-        if (cl) { sh.u.it.yv[k][ph] = xX; sh.u.it.bo[k][ph] = y[0]; }
-        sync_all();
-      }
-      STAMP(4);
-      launder_p();
       const double ei3[3] = {cv[CK_EI0], cv[CK_EI1], cv[CK_EI2]};
       const double dif = cv[CK_DFI], diX = cv[CK_DXI], pbf = cv[CK_PBF], pbx = cv[CK_PBX];
-      const double cinv = cv[CK_CI], csc = cv[CK_C];
-      lds_cd* const YV = (lds_cd*)&sh.u.it.yv[0][0];  // X_{k'} of stage k' >= 1 at 12 (k' - 1)
       double mine, pmine;  // this lane's row maxima (tred6: primal quantity 3 b3 + (b2 ? 2 : b1))
       {  // primal side: A x - z on the own rows
         double ax[3], q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        rowA(xf, xX, YV, ax);
+        rowA(xf, xX, XP, ax);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           const double ei = ei3[j], d = ax[j] - z[j];
@@ -1875,7 +1897,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       {  // dual side: P x + A' y on the own columns
         double q6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         double atf, atX;
-        colAt(y, &sh.u.it.bo[0][0], atf, atX);
+        colAt(y, WD, atf, atX);
         const double pxf = pbf * xf, pxX = pbx * xX;
         const double df_ = pxf + atf, dX_ = pxX + atX;
         if (cl) {
@@ -1891,14 +1913,20 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         mine = tstep(kXor1{}, pmine, tred6(q6, s), s & 1);
       }
       mine = pair_max(row_pair_max(mine));  // the wave's four rows
-      if (lane < 16) sh.red[32 * wv + lane] = mine;
-      sync_all();
-      STAMP(8);
+      if (lane < 16) D[DS * wv + lane] = mine;
+    };
+    // info_combine: the residuals and tolerances (uniform) from every wave's partials in
+    // D (stride DS); INF: the cheap infeasibility partials (slots 16..) into inf_need
+    auto info_combine = [&](auto inf_tag, const double (&cv)[CK_COUNT], const double* const D, int DS)
+        __attribute__((always_inline)) {
+      constexpr bool INF = decltype(inf_tag)::value;
+      MPCQ_CHECK_IDS();
+      const double cinv = cv[CK_CI], csc = cv[CK_C];
       double qv[12];
       {
-        double v = sh.red[s];
+        double v = D[s];
 #pragma unroll
-        for (int w = 1; w < NW; ++w) v = fmax(v, sh.red[32 * w + s]);
+        for (int w = 1; w < NW; ++w) v = fmax(v, D[DS * w + s]);
         qv[0] = rbc<0>(v); qv[1] = rbc<2>(v); qv[2] = rbc<4>(v);
         qv[3] = rbc<8>(v); qv[4] = rbc<10>(v); qv[5] = rbc<12>(v);
         qv[6] = rbc<1>(v); qv[7] = rbc<3>(v); qv[8] = rbc<5>(v);
@@ -1917,10 +1945,10 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       if constexpr (INF) {
         // the cheap conditions of infeas_cheap: slots 0 ||E dy||, 2 ||D dx||, 3 ||D^-1 P dx||, 6 u'dy+ + l'dy-
         const int e = s == 2 || s == 3 || s == 6 ? s : 0;
-        double v = sh.red[16 + e];
+        double v = D[16 + e];
 #pragma unroll
         for (int w = 1; w < NW; ++w) {
-          const double t2 = sh.red[32 * w + 16 + e];
+          const double t2 = D[DS * w + 16 + e];
           v = s == 6 ? v + t2 : fmax(v, t2);
         }
         // kept in VGPRs (every lane holds the same values) and folded into one uniform
@@ -1942,7 +1970,67 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         inf_need = __builtin_amdgcn_readfirstlane(need);
         inf_bits = 0;
       }
+    };
+    // INF: after infeas_cheap, which has published the states / duals with its deltas
+    auto update_info = [&](auto inf_tag, const double (&cv)[CK_COUNT]) __attribute__((always_inline)) {
+      constexpr bool INF = decltype(inf_tag)::value;
+      if constexpr (!INF) {
+        if (cl) { sh.u.it.yv[k][ph] = xX; sh.u.it.bo[k][ph] = y[0]; }
+        sync_all();
+      }
+      STAMP(4);
+      launder_p();
+      info_terms(cv, (lds_cd*)&sh.u.it.yv[0][0], &sh.u.it.bo[0][0], sh.red, 32);
       sync_all();
+      STAMP(8);
+      info_combine(inf_tag, cv, sh.red, 32);
+      sync_all();
+    };
+    // ---- the deferred check (kDC) -----------------------------------------------
+    // the checked iteration's deltas x / y (and dyp) for the products pass, private
+    double dc_mem_[kDC<N> ? 5 : 1];
+    auto dc_ptr = [&]() __attribute__((always_inline)) -> pdbl* {
+      pdbl* q = (pdbl*)&dc_mem_[0];
+      asm volatile("" : "+v"(q));
+      return q;
+    };
+    // at the checked iteration (after its update): publish X / y for the carrier's
+    // residual terms and the cheap infeasibility partials, keep the deltas; no barrier
+    // (the carrier's right-hand-side barrier publishes it all)
+    auto dc_publish = [&](const double (&dy)[3], double dxf, double dxX, const double (&cv)[CK_COUNT])
+        __attribute__((always_inline)) {
+      if constexpr (kDC<N>) {
+        cheap_partials(dy, dxf, dxX, cv, sh.dcp, 24);
+        if (cl) { sh.ckx[k][ph] = xX; sh.u.it.nb[k][ph] = y[0]; }
+        pdbl* const q = dc_ptr();
+        q[0] = dxf; q[1] = dxX; q[2] = dyp[0]; q[3] = dyp[1]; q[4] = dyp[2];
+      }
+    };
+    // in the carrier, after its sweep (waves 1.. while wave 0 sweeps): the residual terms
+    // of the checked iteration, whose x / z / y the carrier has not updated yet
+    auto dc_terms = [&](const double (&cv)[CK_COUNT]) __attribute__((always_inline)) {
+      if constexpr (kDC<N>) {
+        launder_p();
+        info_terms(cv, (lds_cd*)&sh.ckx[0][0], &sh.u.it.nb[0][0], sh.dcp, 24);
+      }
+    };
+    // the products pass of the infeasibility tests for a deferred check (inf_need != 0):
+    // the deltas published where infeas_products reads them (the carrier's sweep is done
+    // with na / nb), the cheap maxima ndy / ndx copied to red, then infeas_products
+    auto dc_products = [&](const double (&cv)[CK_COUNT]) __attribute__((always_inline)) {
+      if constexpr (kDC<N>) {
+        MPCQ_CHECK_IDS();
+        pdbl* const q = dc_ptr();
+        const double dxf = q[0], dxX = q[1];
+        dyp[0] = q[2]; dyp[1] = q[3]; dyp[2] = q[4];
+        if (cl) {
+          sh.u.it.na[k][ph] = dxX;
+          sh.u.it.nb[k][ph] = dyp[0];
+        }
+        if (lane == 0 || lane == 4) sh.red[32 * wv + 16 + (lane >> 1)] = sh.dcp[24 * wv + 16 + (lane >> 1)];
+        sync_all();
+        infeas_products(dxf, dxX, cv);
+      }
     };
     auto converged = [&](double fac) __attribute__((always_inline)) {
       return pri_res < fac * eps_pri && dua_res < fac * eps_dua;
@@ -2765,10 +2853,15 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         // their own without them, so the check / infeasibility code and its live values
         // sit outside the hot loop's register allocation (inside it, they cost 0.31 us
         // per iteration through spills on the sweep path, measured).
-        auto admm_iter = [&](auto delta_tag, const RhsOps& ops, double (&dyv)[3], double& dxf_, double& dxX_,
-                             double (&cvp)[CK_COUNT])
+        // MODE 0: a plain iteration; 1 (DELTA): the checked one, also keeping delta_y / delta_x;
+        // 2 (CARRY, kDC): the iteration after a deferred check, which evaluates that check
+        // between its sweep and its update and returns before the update (*stop = the
+        // status) when it ends the solve
+        auto admm_iter = [&](auto mode_tag, const RhsOps& ops, double (&dyv)[3], double& dxf_, double& dxX_,
+                             double (&cvp)[CK_COUNT], int* stop)
             __attribute__((always_inline)) {
-          constexpr bool DELTA = decltype(delta_tag)::value;
+          constexpr int MODE = decltype(mode_tag)::value;
+          constexpr bool DELTA = MODE == 1, CARRY = MODE == 2;
           double uf, beta, sf, sX, ax[3];
           // (beyond 32 stages the operands are read per iteration: held, they cost the
           // register budget of the 9..16-wave workgroups -- N = 48: scratch 840 -> 712 B
@@ -2778,6 +2871,11 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // DELTA (the last iteration before a check): the check's constant block is read
           // here, its memory latency behind the force recovery and the z / y / x update
           if constexpr (DELTA) ck_all(cvp);
+          // CARRY: the deferred check's residual terms, on waves 1.. while wave 0 sweeps
+          if constexpr (CARRY) {
+            ck_all(cvp);
+            dc_terms(cvp);
+          }
           double zl[3], zh[3], zrr[3], zri[3];  // the update's per-row constants
           if constexpr (kZcMem<N>) {
             ph_recover(nullptr, zc_ptr()[ZC_RI], uf, beta, sf, sX, ax);
@@ -2790,6 +2888,25 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             ph_recover(kBig<N> ? nullptr : &ops, ri[0], uf, beta, sf, sX, ax);
 #pragma unroll
             for (int j = 0; j < 3; ++j) { zl[j] = lo_of(j); zh[j] = hi_of(j); zrr[j] = rr[j]; zri[j] = ri[j]; }
+          }
+          if constexpr (CARRY) {
+            // (ph_recover's barrier published every wave's terms) osqp's check_termination
+            // on the checked iteration, then the infeasibility products where needed
+            info_combine(std::true_type{}, cvp, sh.dcp, 24);
+            int st = 0;
+            if (!(isfinite(pri_res) && isfinite(dua_res))) {
+              st = MPCQ_STATUS_NONFINITE;
+            } else if (converged(1.0)) {
+              st = MPCQ_STATUS_SOLVED;
+            } else {
+              if (inf_need) dc_products(cvp);
+              if (inf_bits & 1) st = MPCQ_STATUS_PRIMAL_INFEASIBLE;
+              else if (inf_bits & 2) st = MPCQ_STATUS_DUAL_INFEASIBLE;
+            }
+            if (st != 0) {
+              *stop = st;
+              return;
+            }
           }
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
@@ -2810,6 +2927,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         };
         const bool chk_on = p.check_termination > 0;
         const bool adp_on = p.adaptive_rho && p.adaptive_rho_interval > 0;
+        bool dc_pending = false;  // (kDC) the previous iteration's check awaits its carrier
         while (iter <= p.max_iter) {
           // the next event: a termination check, an adaptive-rho step or the last iteration
           int until = p.max_iter - iter + 1;
@@ -2821,15 +2939,45 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           RhsOps ops;
           if constexpr (!kBig<N>) load_rhs_ops(ops);
           double cvp[CK_COUNT];
+          int r0 = 1;
+          if constexpr (kDC<N>) {
+            if (dc_pending) {  // this segment's first iteration carries the deferred check
+              dc_pending = false;
+              int st = 0;
+              admm_iter(std::integral_constant<int, 2>{}, ops, dyv, dxf_, dxX_, cvp, &st);
+              if (st != 0) {  // the check of the previous iteration ends the solve there
+                status = st;
+                --iter;
+                break;
+              }
+              r0 = 2;
+              ++iter;
+            }
+          }
 #pragma nounroll
-          for (int r_ = 1; r_ < until; ++r_, ++iter) admm_iter(std::false_type{}, ops, dyv, dxf_, dxX_, cvp);
-          admm_iter(std::true_type{}, ops, dyv, dxf_, dxX_, cvp);
+          for (int r_ = r0; r_ < until; ++r_, ++iter)
+            admm_iter(std::integral_constant<int, 0>{}, ops, dyv, dxf_, dxX_, cvp, nullptr);
+          admm_iter(std::integral_constant<int, 1>{}, ops, dyv, dxf_, dxX_, cvp, nullptr);
           // iter % check_termination == 0 / iter % adaptive_rho_interval == 0, by countdown
           const bool can_check = chk_on && (to_check -= until) == 0;
           if (can_check) to_check = p.check_termination;
           const bool adapt = adp_on && (to_adapt -= until) == 0;
           if (adapt) to_adapt = p.adaptive_rho_interval;
           last_checked = can_check;
+          if constexpr (kDC<N>) {
+            // a check that is not an adaptive-rho step, followed by an iteration that is not
+            // itself an event, is deferred into that iteration (the carrier)
+            int nxt = p.max_iter - iter;
+            if (chk_on && to_check < nxt) nxt = to_check;
+            if (adp_on && to_adapt < nxt) nxt = to_adapt;
+            if (can_check && !adapt && nxt >= 2) {
+              dc_publish(dyv, dxf_, dxX_, cvp);
+              dc_pending = true;
+              STAMP(11);
+              ++iter;
+              continue;
+            }
+          }
           // the last iteration's information is always formed here, while its deltas are
           // live (osqp's update_info after the loop when the last iteration was unchecked)
           infeas_cheap(dyv, dxf_, dxX_, cvp);

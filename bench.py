@@ -5,6 +5,13 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
            --master-port P bench.py --gpus N --steps K --warmup W
 
+Without an external launcher, --gpus N > 1 starts the N rank processes itself
+(mpcq/launch.py: fresh interpreters with RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / MASTER_PORT set, before this process touches the GPU; a
+failing rank stops the others and the exit status is non-zero).  Under a launcher
+WORLD_SIZE must equal --gpus.  RCCL ("nccl") needs a GPU per rank;
+MPCQ_DIST_BACKEND=gloo rehearses more ranks than GPUs.
+
 One step = one launch of the fused engine kernel (formulation + Ruiz scaling +
 KKT factorisation + OSQP ADMM to eps 1e-7) over this rank's batch of
 synthetic (xref, fsteps) instances, inputs resident in HBM.  Ranks shard the

@@ -584,12 +584,19 @@ constexpr bool kCR = false;
 // update, so the result is the checked iteration's -- the same decisions, iteration
 // counts and bits as the blocking check, which stays for the adaptive-rho steps, the
 // last iteration and beyond 32 stages.
-#ifdef MPCQ_NO_DC
-template <int N>
-constexpr bool kDC = false;  // (A/B builds: every check blocking)
-#else
+// Measured and NOT the default (round 4, profiles/r04d_*): the GPU suite passes on it
+// (73/73, same statuses / iterations), but a check costs 4.00 us on the critical path
+// against 3.43 blocking (tools/checkcost.py, N = 16, interval 25), and the unchecked
+// iteration 1.675 vs 1.657 us: wave 0 still forms its own four stages' terms (~400
+// instructions, the bulk of the check) after its sweep, now behind an exposed
+// private-memory load of the constant block; moving them to another wave needs wave 0's
+// x / z / y in LDS (352 doubles at N = 16) where 344 are left.  Build with -DMPCQ_DC.
+#ifdef MPCQ_DC
 template <int N>
 constexpr bool kDC = N <= 32 && !kCR<N>;
+#else
+template <int N>
+constexpr bool kDC = false;
 #endif
 template <int N>
 struct CRL {  // offsets (doubles) of the reduction's arrays (kCR<N>)
@@ -764,7 +771,11 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
   // sweep lane's state index; lanes 12..15 (no state) repeat lanes 0..3, which sit in
   // their bank group, so their reads broadcast instead of conflicting (measured:
   // -2 % per iteration at N <= 16; +2 % at N = 32, which keeps lane 11's)
+#ifdef MPCQ_RR_BCAST
+  int rr_ = s < 12 ? s : s - 12;  // (experiment: the N <= 16 choice at every N)
+#else
   int rr_ = s < 12 ? s : (N <= 16 ? s - 12 : 11);
+#endif
   // store v at q when c holds, else into this lane's sink (branch-free)
   auto launder = [&]() __attribute__((always_inline)) {
     lds_uniform(Ab); lds_uniform(GHr); lds_uniform(SmR); lds_uniform(FWr); lds_uniform(QLr);

@@ -80,8 +80,22 @@ def main():
                      f"{r['Percentage']} % of GPU time")
     if trace:
         t = trace[0]
-        lines.append(f"- launch: grid {t['Grid_Size_X']} threads, workgroup {t['Workgroup_Size_X']}, LDS {t['LDS_Block_Size']} B, "
-                     f"scratch {t['Scratch_Size']} B/lane, arch VGPR {t['VGPR_Count']}, AGPR {t['Accum_VGPR_Count']}, SGPR {t['SGPR_Count']}")
+        lines.append(f"- launch (trace fields): grid {t['Grid_Size_X']} threads, workgroup {t['Workgroup_Size_X']}, "
+                     f"LDS {t['LDS_Block_Size']} B, scratch {t['Scratch_Size']} B/lane; the trace's register fields "
+                     f"(VGPR_Count {t['VGPR_Count']}, Accum_VGPR_Count {t['Accum_VGPR_Count']}, SGPR_Count "
+                     f"{t['SGPR_Count']}) are the dispatch's allocation fields, not the compiler's count (below)")
+    # the compiler's own budget for the profiled horizon (tools/resource_usage.py)
+    try:
+        ru = json.load(open(os.path.join(REPO, "profiles", "resource_usage.json")))
+        N = a.key.split("_N")[1].split("_")[0] if "_N" in a.key else None
+        for kind, v in (ru.get(N) or {}).items():
+            if kind.startswith("fused solve"):
+                lines.append(f"- compiler (`-Rpass-analysis=kernel-resource-usage`, N = {N}, {kind}): VGPRs {v.get('VGPRs')}, "
+                             f"AGPRs {v.get('AGPRs')}, SGPRs {v.get('TotalSGPRs')}, scratch {v.get('ScratchSize')} B/lane, "
+                             f"{v.get('VGPRs Spill')} VGPRs / {v.get('SGPRs Spill')} SGPRs spilled, occupancy "
+                             f"{v.get('Occupancy')} waves/SIMD, LDS {v.get('LDS Size')} B")
+    except (OSError, ValueError, IndexError):
+        pass
     if fk is not None and wk is not None:
         rd_raw, wr = fk * 1024, wk * 1024
         traffic = 2 * rd_raw + wr

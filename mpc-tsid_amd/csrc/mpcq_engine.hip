@@ -769,13 +769,12 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
   int fo = FO<N>(k, f, cc), xo = XO<N>(k, ph);  // own force / state column in Ab
   int cr = (t >> 4) & 1;            // sweep row (wave 0): 0 top-down, 1 bottom-up
   // sweep lane's state index; lanes 12..15 (no state) repeat lanes 0..3, which sit in
-  // their bank group, so their reads broadcast instead of conflicting (measured:
-  // -2 % per iteration at N <= 16; +2 % at N = 32, which keeps lane 11's)
-#ifdef MPCQ_RR_BCAST
-  int rr_ = s < 12 ? s : s - 12;  // (experiment: the N <= 16 choice at every N)
-#else
-  int rr_ = s < 12 ? s : (N <= 16 ? s - 12 : 11);
-#endif
+  // their bank group, so their reads broadcast instead of conflicting (measured: -2 %
+  // per iteration at N <= 16; at N = 32, round 4, same box: SQ_LDS_BANK_CONFLICT per C3
+  // launch 1.375e9 -> 0.718e9, 1.57 -> 0.82 of SQ_ACTIVE_INST_LDS, 3.169 -> 3.128 us per
+  // iteration, C3 33.85 -> 33.35 ms, profiles/r04e_*; round 2's +2 % there is not
+  // reproduced).  Beyond 32 stages (the split sweep) lane 11's row, unmeasured.
+  int rr_ = s < 12 ? s : (N <= 32 ? s - 12 : 11);
   // store v at q when c holds, else into this lane's sink (branch-free)
   auto launder = [&]() __attribute__((always_inline)) {
     lds_uniform(Ab); lds_uniform(GHr); lds_uniform(SmR); lds_uniform(FWr); lds_uniform(QLr);

@@ -8,13 +8,26 @@ robot (whose states are solver outputs); forces and solutions within SOLVE_TOL
 (observed 1.3e-9 after 10 warm-started ticks; the tolerance sits two decades
 above; the virtual robot's states, fed back from the solutions, also get a
 relative 1e-6); status and iteration counts identical on every (robot, tick)
-pair."""
+pair.
+
+Beyond 48 stages the host-fed loop is compared relative to the solution's scale,
+within SCALED_TOL * max(1, max |x|).  Where the difference comes from
+(tools/drift.py, profiles/r04e_drift.txt): one KKT solve differs from the
+oracle's by ~1e-13 of the scale at every horizon (64 as 16); the ADMM iteration
+carries it up transiently after each rho update (N = 64: 2e-12 at iteration 100,
+8e-10 at 200, 4e-11 at convergence; N = 16: 6e-12, 8e-11, 4e-13), and the warm
+start compounds it tick over tick, most for the robots that stop at max_iter
+(unconverged: N = 64 reaches 4000 iterations at most ticks).  Observed on these
+inputs, tick 5, relative to the scale: N = 48 3.2e-9, 49 1.3e-8, 50 1.9e-7, 57
+1.1e-8, 64 2.44e-7 (6.1e-6 absolute, |x| up to 25); SCALED_TOL sits 2x above the
+largest.  Iteration counts stay identical on every (robot, tick)."""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 SOLVE_TOL = 1e-7
+SCALED_TOL = 5e-7  # N > 48, relative to max(1, max |x|) (observed up to 2.44e-7, see above)
 
 
 @pytest.fixture(scope="module")
@@ -52,8 +65,8 @@ def _compare(sess, ors, mpcq, k, agree, plan_tol=1e-15, x_rtol=0.0, scaled=False
     xr = sess.read(mpcq.SV_X_ROBOT)
     for b, o in enumerate(ors):
         ctx = (k, b)
-        # scaled: ten times the tolerance, relative to the solution's scale max(1, max |x|)
-        tol = SOLVE_TOL * (10.0 * max(1.0, float(np.abs(o.x).max())) if scaled else 1.0)
+        # scaled: SCALED_TOL relative to the solution's scale max(1, max |x|)
+        tol = SCALED_TOL * max(1.0, float(np.abs(o.x).max())) if scaled else SOLVE_TOL
         assert st[b] == o.status, ctx
         assert np.array_equal(gait[b], o.planner.gait), ctx
         np.testing.assert_allclose(xref[b], o.planner.xref, rtol=0, atol=plan_tol, err_msg=str(ctx))
@@ -69,7 +82,7 @@ def _compare(sess, ors, mpcq, k, agree, plan_tol=1e-15, x_rtol=0.0, scaled=False
 
 
 @pytest.mark.parametrize("N,dual_warm", [(8, 0), (10, 1), (13, 0), (16, 0), (16, 1), (24, 1), (32, 0), (48, 1),
-                                         (64, 1)])
+                                         (49, 1), (50, 1), (64, 1)])
 def test_session_host_inputs_vs_oracle(mpcq, N, dual_warm):
     """Measured states from the host each tick (the reference's interface), with
     either dual carry-over (dual_warm = 1: osqp's scaled workspace y)."""
@@ -86,10 +99,9 @@ def test_session_host_inputs_vs_oracle(mpcq, N, dual_warm):
             sess.tick(v_ref, state=state, l_feet=l_feet, reduced=red, k=k)
             for b, o in enumerate(ors):
                 o.tick(k, v_ref[b], state=state[b], l_feet=l_feet[b], reduced=bool(red[b]))
-            # N = 64: warm-started rounding grows with the chain and the ticks (observed 7.1e-6 at
-            # tick 5 with |x| up to 25, i.e. 3e-7 of the scale, iteration counts identical):
-            # a scale-relative tolerance
-            d, _ = _compare(sess, ors, mpcq, k, agree, scaled=N > 56)
+            # beyond 48 stages a scale-relative tolerance (module docstring: where the
+            # difference comes from, and what was observed per horizon)
+            d, _ = _compare(sess, ors, mpcq, k, agree, scaled=N > 48)
             worst = max(worst, d)
     assert np.mean(agree) == 1.0
     print(f"N={N}: max |f0 - f0_oracle| over {T} ticks = {worst:.2e}, iteration counts agree {np.mean(agree):.3f}")

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--pick", choices=("slowest", "fastest"), default="slowest",
                     help="which instance of the batch to copy")
     ap.add_argument("--polish", action="store_true", help="the bench's accuracy mode (polish=2 instantiation)")
+    ap.add_argument("--batches", type=int, nargs="+", default=[256, 512, 1024],
+                    help="copies per launch (below 256 some CUs idle: the per-instance share of each XCD's L2 grows)")
     a = ap.parse_args()
     import torch
     import mpcq
@@ -51,7 +53,7 @@ def main():
     r = eng.solve(src["xref"][slow:slow + 1], src["fsteps"][slow:slow + 1])
     print(f"C2 batch: kernel {ms:.3f} ms, iterations median {np.median(its):.0f} max {its.max()} ({a.pick}: instance {slow}, "
           f"{int(r['rho_updates'][0])} rho updates)")
-    for B in (256, 512, 1024):
+    for B in a.batches:
         xr = np.repeat(src["xref"][slow:slow + 1], B, axis=0)
         fs = np.repeat(src["fsteps"][slow:slow + 1], B, axis=0)
         it2, ms2 = run(xr, fs, a.reps)

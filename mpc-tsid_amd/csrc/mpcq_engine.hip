@@ -45,6 +45,11 @@ typedef __attribute__((address_space(3))) const double lds_cd;
 typedef __attribute__((address_space(3))) double lds_d;
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const dbl2 lds_cd2;
+// the per-instance workspace (N > 32) in the global address space: generic (flat)
+// loads would also count in lgkmcnt, so every LDS wait behind them would wait for L2
+typedef __attribute__((address_space(1))) const double g_cd;
+typedef __attribute__((address_space(1))) double g_d;
+typedef __attribute__((address_space(1))) const dbl2 g_cd2;
 
 constexpr double kInf = 1e30;  // OSQP_INFTY
 constexpr double kMinScaling = 1e-4, kMaxScaling = 1e4;
@@ -62,8 +67,10 @@ enum : unsigned { RC_LOOSE = 0, RC_INEQ = 1, RC_EQ = 2 };
 #define STAMP(i) do { if constexpr ((i) == 1 || (i) == 2 || (i) == 3 || (i) == 7 || (i) == 10 || (i) == 11 || (i) == 12) { \
     const uint64_t nw_ = __builtin_amdgcn_s_memtime(); st_acc[i] += nw_ - st_last; st_last = nw_; } } while (0)
 #elif defined(MPCQ_STAMPS)
+// (MPCQ_STAMP_WAVE = w: the stamps of wave w's first lane instead of wave 0's, clamped
+// to the workgroup's last wave: kStampT)
 #define STAMP_DECL uint64_t st_acc[16] = {}; uint64_t st_last = __builtin_amdgcn_s_memtime();
-#define STAMP(i) do { if (threadIdx.x == 0) { const uint64_t nw_ = __builtin_amdgcn_s_memtime(); st_acc[i] += nw_ - st_last; st_last = nw_; } } while (0)
+#define STAMP(i) do { if (threadIdx.x == kStampT) { const uint64_t nw_ = __builtin_amdgcn_s_memtime(); st_acc[i] += nw_ - st_last; st_last = nw_; } } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(i) do {} while (0)
@@ -710,6 +717,10 @@ struct Prologue {
 template <int N, bool FUSED, bool SOLVE, bool POLISH>
 __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p, LaunchArgs a) {
   constexpr int NR = kRows<N>, NW = NR / 4, T = 16 * NR, n = 24 * N, m = 44 * N, nnz = 126 * N - 18, MID = N / 2;
+#ifndef MPCQ_STAMP_WAVE
+#define MPCQ_STAMP_WAVE 0
+#endif
+  [[maybe_unused]] constexpr int kStampT = 64 * (MPCQ_STAMP_WAVE < NW ? MPCQ_STAMP_WAVE : NW - 1);
   // the two chains of the state sweeps: top stages 0..MID-1, bottom N-1..MID+1
   // (BOT stages: MID - 1 for even N, MID for odd N), meeting at stage MID
   constexpr int BOT = N - 1 - MID;
@@ -729,17 +740,17 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
   constexpr bool BIG = kBig<N>, ABG = kAbG<N>, CR = kCR<N>;
   // the scaled constraint values: LDS, or (N > 49) this instance's workspace (the
   // formulation-only launch builds them straight into its Ax output)
-  using acd = std::conditional_t<ABG, const double, lds_cd>;
+  using acd = std::conditional_t<ABG, g_cd, lds_cd>;
   double* AbW;
   if constexpr (ABG) AbW = SOLVE ? a.work + b * Work<N>::SIZE + Work<N>::AB : a.Ax_out + b * nnz;
   else AbW = sh.Ab;
   acd* Ab = (acd*)AbW;
   lds_cd* GHr = (lds_cd*)&sh.GH[0][0];
   // S^{-1}, R^{-1} Q: LDS, or (N > 32) this instance's global workspace; F W: LDS
-  using wcd = std::conditional_t<BIG, const double, lds_cd>;
-  using wdd = std::conditional_t<BIG, double, lds_d>;
+  using wcd = std::conditional_t<BIG, g_cd, lds_cd>;
+  using wdd = std::conditional_t<BIG, g_d, lds_d>;
   wcd* SmR;
-  double* FRg = nullptr;  // (kFrWork: N > 48) this lane's F_k row in the workspace, stride 16 kRows
+  g_d* FRg = nullptr;  // (kFrWork: N > 48) this lane's F_k row in the workspace, stride 16 kRows
   lds_cd* FWr;
   wcd* QLr;
   wdd* SmW;
@@ -748,10 +759,10 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
   int zFW, zQL;  // offsets of a zero block from FWr / QLr (masked reads)
   if constexpr (BIG) {
     double* const wk = SOLVE ? a.work + b * Work<N>::SIZE : nullptr;  // (formulation only: unused)
-    SmW = wk + Work<N>::SM;
+    SmW = (wdd*)(wk + Work<N>::SM);
     FWW = (lds_d*)&sh.FWs[0][0];  // (Work<N>::FW stays reserved, unused)
-    QLW = wk + Work<N>::QL;
-    if (SOLVE) FRg = wk + Work<N>::FR + t;
+    QLW = (wdd*)(wk + Work<N>::QL);
+    if (SOLVE) FRg = (g_d*)(wk + Work<N>::FR + t);
     zFW = (int)(sh.zero - &sh.FWs[0][0]);
     zQL = Work<N>::ZERO - Work<N>::QL;
     if (SOLVE && t < 72) wk[Work<N>::ZERO + t] = 0.0;
@@ -2229,7 +2240,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // the ADMM loop in 24 of the 128 VGPRs
           double frg[12];
           if constexpr (kFrWork<N>) {
-            const double* q = FRg;
+            g_cd* q = FRg;
             asm volatile("" : "+v"(q));
 #pragma unroll
             for (int i = 0; i < 12; ++i) frg[i] = q[16 * NR * i];
@@ -2324,6 +2335,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             if (j <= BOT) return Mb + GS * j;
             return Mb + GS * (cr == 0 ? j : BOT);
           };
+          STAMP(15);  // (diagnostic builds: the own right-hand side, then the wait for the others)
           if (t < 64) row6(rowp(1));
           sync_all();
           STAMP(3);
@@ -2528,6 +2540,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
                                      : (cr == 0 ? (j > 2 ? j : 2) : (j < BOT + 1 ? j : BOT + 1));
             return Mb + GS * jj;
           };
+          if constexpr (!CR) STAMP(15);  // (diagnostic builds: as in ph_sweep_split)
           if (t < 64) row12(rowp(1));
           sync_all();
           STAMP(ST);
@@ -3231,7 +3244,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     }
 #ifdef MPCQ_STAMPS
     STAMP(12);
-    if (t == 0 && a.stamps) {
+    if (t == kStampT && a.stamps) {
       for (int i = 0; i < 16; ++i) a.stamps[b * 16 + i] = st_acc[i];
     }
 #endif

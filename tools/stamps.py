@@ -15,10 +15,15 @@ os.environ.setdefault("MPCQ_LIB_VARIANT", "stamps")
 
 NAMES = ["prologue", "scaling", "factor", "iter:w,b,u,beta,bt", "chk:publish", "chk:primal", "iter:inward sweeps+S^-1 y",
          "iter:outward sweeps", "chk:dual", "iter:forces", "iter:z/y/x update", "chk:reduce+adapt", "epilogue", "fac:phaseP", "fac:phaseS"]
+# bucket 15 (round 4): the right-hand-side phase's own work up to its barrier; bucket 3 is
+# then the wait at that barrier (the slowest wave's lag).  MPCQ_STAMP_WAVE=w builds
+# (tools/build_variant.sh, MPCQ_LIB_VARIANT=exp:<name>) stamp wave w instead of wave 0.
+NAMES = NAMES + ["iter:w,b,u,beta,bt (own)"]
+NAMES[3] = "iter:rhs barrier wait"
 # the cyclic-reduction build (kCR horizons): bucket 3 is ph_rhs + its barrier, 15 the
 # reduction of b + its barrier, 12 the outward sweep + the barrier after it, 7 the
 # back-substitution of the odd stages + ph_recover's barrier
-NAMES_CR = list(NAMES) + ["cr:reduce b + barrier"]
+NAMES_CR = list(NAMES[:15]) + ["cr:reduce b + barrier"]
 NAMES_CR[3] = "iter:w,b,u,beta + barrier"
 NAMES_CR[7] = "cr:odd stages + barrier"
 NAMES_CR[12] = "iter:outward + barrier (+epilogue)"
@@ -54,7 +59,7 @@ def main():
     S = stamps.cpu().numpy().astype(np.float64)
     its = it.cpu().numpy()
     names = NAMES_CR if a.cr else NAMES
-    tot = S[:, :13].sum(axis=1) + (S[:, 15] if a.cr else 0.0)
+    tot = S[:, :13].sum(axis=1) + S[:, 15]
     print(f"batch {a.batch} N={a.N}: iters median {np.median(its)} max {its.max()}; "
           f"kernel ms (event) {eng.last_kernel_ms()[1]:.2f}")
     print(f"cycles per instance: median {np.median(tot):.3e}; per iteration {np.median(tot / its):.0f}")

@@ -651,6 +651,17 @@ template <int N> constexpr bool kZcMem = false;
 #else
 template <int N> constexpr bool kZcMem = N > 48;
 #endif
+// The outward sweep of ph_sweep_split (33..48 stages) as ph_sweep_lag's: full 12-term
+// column products per lane (the outward sweep needs no S^{-1}, which is what sent the
+// split sweep's inward half to the stage-parallel S^{-1} phase).  Round 4 (r04h, per
+// iteration alone / 256 in flight): N = 40 6.07 -> 5.93 / 6.94 -> 6.73 us, N = 48 6.89 ->
+// 6.79 / 7.69 -> 7.62; beyond 48 stages mixed (N = 64 14.96 -> 14.78 / 18.73 -> 19.55), so
+// the split products stay there.  -DMPCQ_SPLIT_OUT: the split outward products everywhere.
+#ifdef MPCQ_SPLIT_OUT
+template <int N> constexpr bool kLagOut = false;
+#else
+template <int N> constexpr bool kLagOut = N <= 48;
+#endif
 template <int N>
 struct Work {  // offsets (doubles) inside one instance's workspace
   // SM starts two slots in (a pad kept from round 2; the sweep no longer reads it)
@@ -2343,6 +2354,9 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // slot N-j): column rr, entries h6..h6+5 (LDS offsets are unsigned, so the bases
           // sit at the lowest slot a chain reaches)
           lds_cd* const Ob = GHr + (GS * (cr == 0 ? 1 : N - MID) + (cr == 0 ? 0 : kSlotPad<N>) + rr_ + RS * h6);
+          // (kLagOut) the same columns read whole: lane rr takes all 12 entries of column rr
+          [[maybe_unused]] lds_cd* const ObL = GHr + (GS * (cr == 0 ? 1 : N - MID) + (cr == 0 ? 0 : kSlotPad<N>) + rr_);
+          [[maybe_unused]] double go[kLagOut<N> ? 12 : 1];
           if (t < 64) {
             // the sweeps are every wave's critical path (the other waves of the instance
             // wait at the barrier): issue them ahead of a co-resident instance's phases
@@ -2385,6 +2399,9 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
                 row6(GHr + RS * rr_ + h6);
                 lds_cd* qb = (lds_cd*)&sh.u.it.bo[MID][ri];
                 b0 = qb[0]; b1 = qb[12 * N];
+              } else if constexpr (kLagOut<N>) {  // the last step: the first outward step's columns (12 terms)
+#pragma unroll
+                for (int i = 0; i < 12; ++i) go[i] = ObL[RS * i + GS * (MID - 1)];
               } else {  // the last step: the first outward step's columns
 #pragma unroll
                 for (int i = 0; i < 6; ++i) g[i] = Ob[RS * i + GS * (MID - 1)];
@@ -2415,7 +2432,10 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
                 const bool adv = j <= BOT || cr == 0;
                 src = adv ? yb : src;
               } else {
-                xp = yb;
+                // (kLagOut: the outward products are full rows on every row pair, so every
+                // row takes x_m in its own layout; pair_sum32 left it bit-identical in rows
+                // 0 / 2 and 1 / 3)
+                xp = kLagOut<N> ? y : yb;
                 if (cr == 0 && hi == 0 && s < 12) sh.u.it.xs[SIGX<N>(MID + 1)][rr_] = y;
               }
             }
@@ -2453,6 +2473,34 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             lds_d* const Xb = (hi == 0 && s < 12) ? (lds_d*)&sh.u.it.xs[0][0] + (12 * (cr == 0 ? 1 : N - MID) + rr_)
                                                   : sinkO;
             double bq = Wb[12 * (MID - 1)];
+            if constexpr (kLagOut<N>) {
+              // full 12-term column products on every row (rows 2 / 3 repeat rows 0 / 1): one
+              // v_fmac chain per step, no swap-add, rotation or select (as ph_sweep_lag)
+#pragma unroll
+              for (int j = 1; j <= MID; ++j) {
+                asm volatile("" : : : "memory");
+                double gc[12];
+#pragma unroll
+                for (int i = 0; i < 12; ++i) gc[i] = go[i];
+                const double bc = bq;
+                if (j < MID) {
+#pragma unroll
+                  for (int i = 0; i < 12; ++i) go[i] = ObL[RS * i + GS * (MID - j - 1)];
+                  if (j + 1 <= BOT) bq = Wb[12 * (MID - j - 1)];
+                  else bq = Wb[12 * (MID - (cr == 0 ? j + 1 : BOT))];
+                }
+                asm volatile("" : : : "memory");
+                const double acc = bdot12(gc, xp, bc);  // x = w - G' x_next with -G stored
+                if (j < MID) {
+                  xp = acc;
+                  Xb[12 * (MID - j)] = acc;
+                } else if constexpr (N & 1) {
+                  *Xb = acc;
+                } else {
+                  *(cr == 0 ? Xb : sinkO) = acc;
+                }
+              }
+            } else {
 #pragma unroll
             for (int j = 1; j <= MID; ++j) {
               asm volatile("" : : : "memory");
@@ -2479,6 +2527,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               } else {  // even N: the bottom chain has no step MID
                 *(cr == 0 ? Xb : sinkO) = x;
               }
+            }
             }
             __builtin_amdgcn_s_setprio(0);
           }

@@ -136,6 +136,30 @@ def test_planner_vs_oracle_random(mpcq, engines, N):
     assert bad_seen > 0  # malformed tables were exercised
 
 
+@pytest.mark.parametrize("N,B", [(16, 7), (31, 5), (31, 64), (8, 1)])
+def test_planner_half_wave_edges(mpcq, N, B):
+    """Up to N = 31 two instances share a wave64 (32 lanes each): odd batches leave the
+    last wave's second half empty, N = 31 fills every lane of a half with a column.
+    Every op sequence of the random test, against the oracle."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(900 + 10 * N + B)
+    gait, state, l_feet, v_ref, reduced = _random_batch(rng, B, N)
+    bs = BatchState(gait, N)
+    ors = [O.Planner(N, gait[b]) for b in range(B)]
+    with mpcq.Engine(N) as eng:
+        for j, ops in enumerate((mpcq.PLAN_TICK, mpcq.PLAN_ROLL | mpcq.PLAN_FOOTSTEPS, mpcq.PLAN_REFSTATES,
+                                 mpcq.PLAN_TICK)):
+            st = bs.plan(eng, ops, j, state, l_feet, v_ref, reduced=reduced)
+            for b in range(B):
+                so = ors[b].plan(ops, j, state[b], l_feet[b], v_ref[b], reduced=bool(reduced[b]))
+                assert st[b] == so, (j, b)
+            assert np.array_equal(bs.gait, np.stack([o.gait for o in ors])), j
+            assert np.array_equal(bs.rot_flag, np.concatenate([o.flag for o in ors])), j
+            _close(bs.fsteps, np.stack([o.fsteps for o in ors]))
+            _close(bs.xref, np.stack([o.xref for o in ors]))
+            state = state + rng.normal(0, 0.01, state.shape)
+
+
 def test_planner_api_errors(mpcq, engines):
     eng = engines[16]
     bs = BatchState(np.zeros((2, 20, 5)), 16)

@@ -697,7 +697,8 @@ struct Smem {
       double xs[N + 1][12];  // X_k (xs[k+1] = X_{k+1}, stage k's states)
     } it;
     struct {
-      double St[144], Sb[144];  // sweep hand-offs of the factorisation
+      alignas(16) double St[144];  // sweep hand-offs of the factorisation (16-B aligned: the
+      alignas(16) double Sb[144];  // couplings read them as column pairs)
       double Lm[144];           // (kCR) the reduced meeting row's lower coupling
     } fa;
   } u;
@@ -1268,20 +1269,25 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         const double* const Sp = upper ? St : Sb;
         wave_sync();  // this row's reads of GH[k], GH[k+1] are done
         const int ar = ph < 6 ? ph : ph - 6;
-        // column by column: the seven operands of one column are loaded together
-        // and waited for once (row blocks waited load by load under the register
-        // pressure here)
+        // two columns at a time: their fourteen operands as seven 16-B reads, loaded
+        // together and waited for once, and two independent FMA chains (each column's
+        // sum in the same order as one at a time; row blocks waited load by load under
+        // the register pressure here)
         double G[12];
 #pragma unroll
-        for (int ci = 0; ci < 12; ++ci) {
-          double sv[7];
-          sv[0] = Sp[12 * ar + ci];
+        for (int ci = 0; ci < 12; ci += 2) {
+          const dbl2 s0 = *(lds_cd2*)(Sp + 12 * ar + ci);
+          dbl2 su[6];
 #pragma unroll
-          for (int j = 0; j < 6; ++j) sv[1 + j] = Sp[12 * (6 + j) + ci];
-          double gv = ca * sv[0];
+          for (int j = 0; j < 6; ++j) su[j] = *(lds_cd2*)(Sp + 12 * (6 + j) + ci);
+          double g0 = ca * s0.x, g1 = ca * s0.y;
 #pragma unroll
-          for (int j = 0; j < 6; ++j) gv = fma(c6[j], sv[1 + j], gv);
-          G[ci] = gv;
+          for (int j = 0; j < 6; ++j) {
+            g0 = fma(c6[j], su[j].x, g0);
+            g1 = fma(c6[j], su[j].y, g1);
+          }
+          G[ci] = g0;
+          G[ci + 1] = g1;
           asm volatile("" ::: "memory");
         }
         if (cl) {

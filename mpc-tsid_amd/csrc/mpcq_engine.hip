@@ -311,6 +311,204 @@ __device__ __forceinline__ double sel3(int i, double a0, double a1, double a2) {
 
 // Gauss-Jordan inverse of a 12x12 SPD matrix held one row per column lane
 // (row psi in lane LN(psi)); pivots broadcast by row_newbcast, no pivoting.
+// gj_fmac<PV>: the pivot's eleven row updates c[j] += a * R[j](lane LN(PV)), j != PV, as
+// v_fmac_f64_dpp (the broadcast folded into the FMA: one instruction per entry instead of
+// a DPP move and an FMA; fma(a, b, c) and c += b a round alike, so the same bits)
+template <int PV>
+__device__ __forceinline__ void gj_fmac(double (&c)[12], const double (&R)[12], double a) {
+  if constexpr (PV == 0) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
+        : "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
+  }
+  else if constexpr (PV == 1) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(c[0]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
+        : "v"(R[0]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
+  }
+  else if constexpr (PV == 2) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(c[0]), "+v"(c[1]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
+        : "v"(R[0]), "v"(R[1]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
+  }
+  else if constexpr (PV == 3) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
+        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
+  }
+  else if constexpr (PV == 4) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
+        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
+  }
+  else if constexpr (PV == 5) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
+        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
+  }
+  else if constexpr (PV == 6) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
+        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
+  }
+  else if constexpr (PV == 7) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
+        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
+  }
+  else if constexpr (PV == 8) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
+        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
+  }
+  else if constexpr (PV == 9) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[10]), "+v"(c[11])
+        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[10]), "v"(R[11]), "v"(a));
+  }
+  else if constexpr (PV == 10) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[11])
+        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[11]), "v"(a));
+  }
+  else if constexpr (PV == 11) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10])
+        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(a));
+  }
+}
 template <int PV>
 __device__ __forceinline__ void gj_step(double (&R)[12], int me, bool& ok) {
   const double d = rbc<LN(PV)>(R[PV]);
@@ -329,12 +527,13 @@ __device__ __forceinline__ void gj_step(double (&R)[12], int me, bool& ok) {
   // R - (R[PV] / d) p, so each entry is a single FMA on the broadcast pivot row
   const bool isp = me == PV;
   const double a = isp ? id : -(R[PV] * id);
+  double c[12];
 #pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    if (j == PV) continue;
-    const double base = isp ? 0.0 : R[j];
-    R[j] = fma(a, rbc<LN(PV)>(R[j]), base);
-  }
+  for (int j = 0; j < 12; ++j) c[j] = isp ? 0.0 : R[j];
+  gj_fmac<PV>(c, R, a);
+#pragma unroll
+  for (int j = 0; j < 12; ++j)
+    if (j != PV) R[j] = c[j];
   R[PV] = a;
 }
 template <int... P>
@@ -348,18 +547,44 @@ __device__ __forceinline__ void gj12(double (&R)[12], int me, bool& ok) {
 // Ro -= G C' for one 12x12 coupling block C held one row per column lane in
 // compact form (ca on column CI mod 6, c6 on the velocity columns): column CI of
 // the product takes row CI of C from lane LN(CI) by row broadcast
+// The broadcasts fold into v_fmac_f64_dpp (one instruction per term instead of a DPP
+// move and an FMA); the two chains start from -0 (x + -0 = x for every x, so the first
+// term is the plain product, as a multiply) and keep their order: the same bits.
+#define MPCQ_SCHUR2_LANE(J)                                                                  \
+  asm("s_nop 1\n\t"                                                                          \
+      "v_fmac_f64_dpp %0, %2, %8 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"        \
+      "v_fmac_f64_dpp %1, %3, %9 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"        \
+      "v_fmac_f64_dpp %0, %4, %10 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %1, %5, %11 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %0, %6, %12 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %1, %7, %13 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %0, %14, %15 row_newbcast:" #J " row_mask:0xf bank_mask:0xf"           \
+      : "+v"(a0), "+v"(a1)                                                                   \
+      : "v"(ca), "v"(c6[0]), "v"(c6[1]), "v"(c6[2]), "v"(c6[3]), "v"(c6[4]), "v"(ga), "v"(G[6]), \
+        "v"(G[7]), "v"(G[8]), "v"(G[9]), "v"(G[10]), "v"(c6[5]), "v"(G[11]))
 template <int CI>
 __device__ __forceinline__ void schur_col(double (&Ro)[12], const double (&G)[12], double ca,
                                           const double (&c6)[6]) {
   constexpr int J = LN(CI);
-  double a0 = G[CI < 6 ? CI : CI - 6] * rbc<J>(ca), a1 = G[6] * rbc<J>(c6[0]);
-  a0 = fma(G[7], rbc<J>(c6[1]), a0);
-  a1 = fma(G[8], rbc<J>(c6[2]), a1);
-  a0 = fma(G[9], rbc<J>(c6[3]), a0);
-  a1 = fma(G[10], rbc<J>(c6[4]), a1);
-  a0 = fma(G[11], rbc<J>(c6[5]), a0);
+  const double ga = G[CI < 6 ? CI : CI - 6];
+  // a0 = ga ca + G7 c1 + G9 c3 + G11 c5, a1 = G6 c0 + G8 c2 + G10 c4 (c broadcast from lane J)
+  double a0 = -0.0, a1 = -0.0;
+  if constexpr (J == 0) MPCQ_SCHUR2_LANE(0);
+  else if constexpr (J == 1) MPCQ_SCHUR2_LANE(1);
+  else if constexpr (J == 2) MPCQ_SCHUR2_LANE(2);
+  else if constexpr (J == 4) MPCQ_SCHUR2_LANE(4);
+  else if constexpr (J == 5) MPCQ_SCHUR2_LANE(5);
+  else if constexpr (J == 6) MPCQ_SCHUR2_LANE(6);
+  else if constexpr (J == 8) MPCQ_SCHUR2_LANE(8);
+  else if constexpr (J == 9) MPCQ_SCHUR2_LANE(9);
+  else if constexpr (J == 10) MPCQ_SCHUR2_LANE(10);
+  else if constexpr (J == 12) MPCQ_SCHUR2_LANE(12);
+  else if constexpr (J == 13) MPCQ_SCHUR2_LANE(13);
+  else if constexpr (J == 14) MPCQ_SCHUR2_LANE(14);
+  else static_assert(J < 0, "a column lane LN(i)");
   Ro[CI] -= a0 + a1;
 }
+#undef MPCQ_SCHUR2_LANE
 template <int... C>
 __device__ __forceinline__ void schur_cols(double (&Ro)[12], const double (&G)[12], double ca,
                                            const double (&c6)[6], std::integer_sequence<int, C...>) {

@@ -314,201 +314,49 @@ __device__ __forceinline__ double sel3(int i, double a0, double a1, double a2) {
 // gj_fmac<PV>: the pivot's eleven row updates c[j] += a * R[j](lane LN(PV)), j != PV, as
 // v_fmac_f64_dpp (the broadcast folded into the FMA: one instruction per entry instead of
 // a DPP move and an FMA; fma(a, b, c) and c += b a round alike, so the same bits)
+#define MPCQ_GJ11(J)                                                                         \
+  asm("s_nop 1\n\t"                                                                          \
+      "v_fmac_f64_dpp %0, %11, %22 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %1, %12, %22 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %2, %13, %22 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %3, %14, %22 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %4, %15, %22 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %5, %16, %22 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %6, %17, %22 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %7, %18, %22 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %8, %19, %22 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %9, %20, %22 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"       \
+      "v_fmac_f64_dpp %10, %21, %22 row_newbcast:" #J " row_mask:0xf bank_mask:0xf"          \
+      : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]), "+v"(o[4]), "+v"(o[5]), "+v"(o[6]),  \
+        "+v"(o[7]), "+v"(o[8]), "+v"(o[9]), "+v"(o[10])                                      \
+      : "v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]), \
+        "v"(r[8]), "v"(r[9]), "v"(r[10]), "v"(a))
 template <int PV>
 __device__ __forceinline__ void gj_fmac(double (&c)[12], const double (&R)[12], double a) {
-  if constexpr (PV == 0) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
-        : "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
+  constexpr int J = LN(PV);
+  double o[11], r[11];  // the entries j != PV in order (register renames, no moves)
+#pragma unroll
+  for (int q = 0; q < 11; ++q) {
+    o[q] = c[q < PV ? q : q + 1];
+    r[q] = R[q < PV ? q : q + 1];
   }
-  else if constexpr (PV == 1) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(c[0]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
-        : "v"(R[0]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
-  }
-  else if constexpr (PV == 2) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(c[0]), "+v"(c[1]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
-        : "v"(R[0]), "v"(R[1]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
-  }
-  else if constexpr (PV == 3) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
-        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
-  }
-  else if constexpr (PV == 4) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
-        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
-  }
-  else if constexpr (PV == 5) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
-        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
-  }
-  else if constexpr (PV == 6) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
-        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
-  }
-  else if constexpr (PV == 7) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
-        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
-  }
-  else if constexpr (PV == 8) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
-        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[9]), "v"(R[10]), "v"(R[11]), "v"(a));
-  }
-  else if constexpr (PV == 9) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[10]), "+v"(c[11])
-        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[10]), "v"(R[11]), "v"(a));
-  }
-  else if constexpr (PV == 10) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[11])
-        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[11]), "v"(a));
-  }
-  else if constexpr (PV == 11) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %11, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %13, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %15, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %17, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %18, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %19, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %20, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %21, %22 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10])
-        : "v"(R[0]), "v"(R[1]), "v"(R[2]), "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]), "v"(R[9]), "v"(R[10]), "v"(a));
-  }
+  if constexpr (J == 0) MPCQ_GJ11(0);
+  else if constexpr (J == 1) MPCQ_GJ11(1);
+  else if constexpr (J == 2) MPCQ_GJ11(2);
+  else if constexpr (J == 4) MPCQ_GJ11(4);
+  else if constexpr (J == 5) MPCQ_GJ11(5);
+  else if constexpr (J == 6) MPCQ_GJ11(6);
+  else if constexpr (J == 8) MPCQ_GJ11(8);
+  else if constexpr (J == 9) MPCQ_GJ11(9);
+  else if constexpr (J == 10) MPCQ_GJ11(10);
+  else if constexpr (J == 12) MPCQ_GJ11(12);
+  else if constexpr (J == 13) MPCQ_GJ11(13);
+  else if constexpr (J == 14) MPCQ_GJ11(14);
+  else static_assert(J < 0, "a column lane LN(i)");
+#pragma unroll
+  for (int q = 0; q < 11; ++q) c[q < PV ? q : q + 1] = o[q];
 }
+#undef MPCQ_GJ11
 template <int PV>
 __device__ __forceinline__ void gj_step(double (&R)[12], int me, bool& ok) {
   const double d = rbc<LN(PV)>(R[PV]);

@@ -3,7 +3,4 @@ cd $GRAFT_REPO_ROOT
 # r04n: the round-4 final build -- GPU suite, smoke, every bench line, the rocprof passes, stamps
 timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/r04n_pytest_gpu.log 2>&1 &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04n_smoke.log 2>&1 &&
-bash tools/bench_all.sh r04n &&
-for n in 16 32; do
-  timeout -k 10 120 python -u tools/stamps.py --N $n --batch 256 > gpurun_out/r04n_stamps$n.txt 2>&1 || exit 1
-done
+bash tools/bench_all.sh r04n

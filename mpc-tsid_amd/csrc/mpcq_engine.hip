@@ -357,7 +357,10 @@ __device__ __forceinline__ void gj_fmac(double (&c)[12], const double (&R)[12], 
   for (int q = 0; q < 11; ++q) c[q < PV ? q : q + 1] = o[q];
 }
 #undef MPCQ_GJ11
-template <int PV>
+// FOLD = false (beyond 32 stages): the DPP move + FMA form -- the folded blocks hold all
+// their operands at once, which the 168 / 128-VGPR budgets there pay for in spills inside
+// the ADMM loop (N = 48: 6 -> 15 scratch reloads per iteration in the gfx950 assembly)
+template <int PV, bool FOLD>
 __device__ __forceinline__ void gj_step(double (&R)[12], int me, bool& ok) {
   const double d = rbc<LN(PV)>(R[PV]);
 #ifdef MPCQ_DEBUG_PIVOT
@@ -375,21 +378,31 @@ __device__ __forceinline__ void gj_step(double (&R)[12], int me, bool& ok) {
   // R - (R[PV] / d) p, so each entry is a single FMA on the broadcast pivot row
   const bool isp = me == PV;
   const double a = isp ? id : -(R[PV] * id);
-  double c[12];
+  if constexpr (FOLD) {
+    double c[12];
 #pragma unroll
-  for (int j = 0; j < 12; ++j) c[j] = isp ? 0.0 : R[j];
-  gj_fmac<PV>(c, R, a);
+    for (int j = 0; j < 12; ++j) c[j] = isp ? 0.0 : R[j];
+    gj_fmac<PV>(c, R, a);
 #pragma unroll
-  for (int j = 0; j < 12; ++j)
-    if (j != PV) R[j] = c[j];
+    for (int j = 0; j < 12; ++j)
+      if (j != PV) R[j] = c[j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      if (j == PV) continue;
+      const double base = isp ? 0.0 : R[j];
+      R[j] = fma(a, rbc<LN(PV)>(R[j]), base);
+    }
+  }
   R[PV] = a;
 }
-template <int... P>
+template <bool FOLD, int... P>
 __device__ __forceinline__ void gj_seq(double (&R)[12], int me, bool& ok, std::integer_sequence<int, P...>) {
-  (gj_step<P>(R, me, ok), ...);
+  (gj_step<P, FOLD>(R, me, ok), ...);
 }
+template <bool FOLD>
 __device__ __forceinline__ void gj12(double (&R)[12], int me, bool& ok) {
-  gj_seq(R, me, ok, std::make_integer_sequence<int, 12>{});
+  gj_seq<FOLD>(R, me, ok, std::make_integer_sequence<int, 12>{});
 }
 
 // Ro -= G C' for one 12x12 coupling block C held one row per column lane in
@@ -410,10 +423,20 @@ __device__ __forceinline__ void gj12(double (&R)[12], int me, bool& ok) {
       : "+v"(a0), "+v"(a1)                                                                   \
       : "v"(ca), "v"(c6[0]), "v"(c6[1]), "v"(c6[2]), "v"(c6[3]), "v"(c6[4]), "v"(ga), "v"(G[6]), \
         "v"(G[7]), "v"(G[8]), "v"(G[9]), "v"(G[10]), "v"(c6[5]), "v"(G[11]))
-template <int CI>
+template <int CI, bool FOLD>
 __device__ __forceinline__ void schur_col(double (&Ro)[12], const double (&G)[12], double ca,
                                           const double (&c6)[6]) {
   constexpr int J = LN(CI);
+  if constexpr (!FOLD) {  // (beyond 32 stages, as gj_step)
+    double a0 = G[CI < 6 ? CI : CI - 6] * rbc<J>(ca), a1 = G[6] * rbc<J>(c6[0]);
+    a0 = fma(G[7], rbc<J>(c6[1]), a0);
+    a1 = fma(G[8], rbc<J>(c6[2]), a1);
+    a0 = fma(G[9], rbc<J>(c6[3]), a0);
+    a1 = fma(G[10], rbc<J>(c6[4]), a1);
+    a0 = fma(G[11], rbc<J>(c6[5]), a0);
+    Ro[CI] -= a0 + a1;
+    return;
+  }
   const double ga = G[CI < 6 ? CI : CI - 6];
   // a0 = ga ca + G7 c1 + G9 c3 + G11 c5, a1 = G6 c0 + G8 c2 + G10 c4 (c broadcast from lane J)
   double a0 = -0.0, a1 = -0.0;
@@ -433,10 +456,10 @@ __device__ __forceinline__ void schur_col(double (&Ro)[12], const double (&G)[12
   Ro[CI] -= a0 + a1;
 }
 #undef MPCQ_SCHUR2_LANE
-template <int... C>
+template <bool FOLD, int... C>
 __device__ __forceinline__ void schur_cols(double (&Ro)[12], const double (&G)[12], double ca,
                                            const double (&c6)[6], std::integer_sequence<int, C...>) {
-  (schur_col<C>(Ro, G, ca, c6), ...);
+  (schur_col<C, FOLD>(Ro, G, ca, c6), ...);
 }
 // i0 + sum_m c_m(lane J) g_m: twelve registers broadcast from one lane J of the row, the
 // broadcast folded into v_fmac_f64_dpp (as one asm block the compiler cannot hoist the
@@ -1278,7 +1301,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           }
           Fr[psi] = v;
         }
-        gj12(Fr, ph, ok);
+        gj12<!kBig<N>>(Fr, ph, ok);
         if constexpr (kFrWork<N>) {
 #pragma unroll
           for (int i = 0; i < 12; ++i) FRg[16 * NR * i] = Fr[i];
@@ -1347,6 +1370,20 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         // sum in the same order as one at a time; row blocks waited load by load under
         // the register pressure here)
         double G[12];
+        if constexpr (kBig<N>) {  // (beyond 32 stages one column at a time, as gj_step)
+#pragma unroll
+          for (int ci = 0; ci < 12; ++ci) {
+            double sv[7];
+            sv[0] = Sp[12 * ar + ci];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) sv[1 + j] = Sp[12 * (6 + j) + ci];
+            double gv = ca * sv[0];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) gv = fma(c6[j], sv[1 + j], gv);
+            G[ci] = gv;
+            asm volatile("" ::: "memory");
+          }
+        } else {
 #pragma unroll
         for (int ci = 0; ci < 12; ci += 2) {
           const dbl2 s0 = *(lds_cd2*)(Sp + 12 * ar + ci);
@@ -1363,12 +1400,13 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           G[ci + 1] = g1;
           asm volatile("" ::: "memory");
         }
+        }
         if (cl) {
           double* const Gd = gh0 + SLOT<N>(upper ? SIG<N>(k) : SIG<N>(k + 1)) + RS * ph;
 #pragma unroll
           for (int ci = 0; ci < 12; ++ci) Gd[ci] = -G[ci];  // stored negated
         }
-        schur_cols(Ro, G, ca, c6, std::make_integer_sequence<int, 12>{});
+        schur_cols<!kBig<N>>(Ro, G, ca, c6, std::make_integer_sequence<int, 12>{});
       };
       if constexpr (CR) {
         // ---- cyclic reduction (kCR): D_o^{-1} of the odd stages, the reduced system
@@ -1392,7 +1430,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           double Ro[12];
 #pragma unroll
           for (int ci = 0; ci < 12; ++ci) Ro[ci] = Dr0[ci];
-          gj12(Ro, ph, ok);
+          gj12<!kBig<N>>(Ro, ph, ok);
           if (cl) {
             double* const q = gh0 + CRL<N>::DI + GS * (k >> 1) + RS * ph;
 #pragma unroll
@@ -1526,7 +1564,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               }
               couple_dn(C, Sb, gh0 + SLOT<NS>(SIG<NS>(j + 1)) + RS * ph, Ro);
             }
-            gj12(Ro, ph, ok);
+            gj12<!kBig<N>>(Ro, ph, ok);
             wave_sync();  // the row's reads of its coupling slot are done
             if (cl) {
 #pragma unroll
@@ -1556,7 +1594,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           for (int ci = 0; ci < 12; ++ci) Ro[ci] = Dr0[ci];
           if (useT) couple(true, Ro);
           if (useB) couple(false, Ro);
-          gj12(Ro, ph, ok);
+          gj12<!kBig<N>>(Ro, ph, ok);
           if (cl) {
 #pragma unroll
             for (int ci = 0; ci < 12; ++ci) SmW[SLOT<N>(SIG<N>(k)) + RS * ph + ci] = Ro[ci];

@@ -117,6 +117,10 @@ def main():
             if name.startswith("SQ_WAIT") or name.startswith("SQ_ACTIVE_INST"):
                 extra += f", {100 * v / cyc:.1f} % of wave cycles" if cyc else ""
             lines.append(f"- {name}: {v:.4g}{extra}")
+        bc, al = mean(sq.get("SQ_LDS_BANK_CONFLICT", [])), mean(sq.get("SQ_ACTIVE_INST_LDS", []))
+        if bc is not None and al:
+            lines.append(f"- SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS = {bc / al:.3f} (conflict cycles per active LDS "
+                         "instruction cycle)")
     fp64_flops = None
     if f64:
         fma, add, mul = (mean(f64.get(n, [])) or 0.0 for n in

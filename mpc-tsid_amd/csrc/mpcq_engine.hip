@@ -758,6 +758,15 @@ template <int N> constexpr bool kLagOut = false;
 #else
 template <int N> constexpr bool kLagOut = N <= 48;
 #endif
+// Stage stride of F W in LDS (doubles).  ph_recover reads row ph of F_k W_k as three
+// ds_read_b128 per lane (16-B units 36 k + 3 ph at a 72-double stride): within each
+// 16-lane bank group of that instruction (two stages' lanes), ph 0/1/2 of one stage met
+// ph 6/7/8 of the next in the same banks (2-way conflicts); at a 96-double stride (256 B
+// x 3, stages 0 mod 16 units apart) the twelve rows of each group land in distinct banks.
+// Up to 32 stages, where the LDS has the 24 N doubles (N = 16: 80,048 B, still two
+// instances per CU); not with the deferred check's extra LDS (kDC).
+template <int N>
+constexpr int kFWS = (N <= 32 && !kDC<N>) ? 96 : 72;
 template <int N>
 struct Work {  // offsets (doubles) inside one instance's workspace
   // SM starts two slots in (a pad kept from round 2; the sweep no longer reads it)
@@ -779,7 +788,7 @@ struct Smem {
   // (N > 32: these three live in the global workspace, Work<N>)
   alignas(16) double Sm[kBig<N> ? 1 : N][GS];  // S_k^{-1} / U_k^{-1} of stage k at SLOT(SIG(k)), row-major (row stride RS)
   double Smpad[2];
-  double FWs[N][72];  // F_k W_k (12x6, row psi at [6 psi]); W_k = B_k' R on rows 6..11
+  alignas(16) double FWs[N][kFWS<N>];  // F_k W_k (12x6, row psi at [6 psi]; stage stride kFWS); W_k = B_k' R on rows 6..11
   double QL[kBig<N> ? 1 : N][36];   // B_k F_k W_k = R^{-1} W_k' F_k W_k (6x6)
   union {
     struct {
@@ -1320,7 +1329,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         }
         if (cl) {
 #pragma unroll
-          for (int j = 0; j < 6; ++j) { gk[36 + 6 * ph + j] = fw[j]; FWW[72 * k + 6 * ph + j] = fw[j]; }
+          for (int j = 0; j < 6; ++j) { gk[36 + 6 * ph + j] = fw[j]; FWW[kFWS<N> * k + 6 * ph + j] = fw[j]; }
         }
         wave_sync();
         // Q = W' (F W): 36 entries over the row's 16 lanes
@@ -1659,8 +1668,8 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       o.oFa = FO<N>(k, f, ta >> 1) + 5 + (ta & 1);
       o.oFb = FO<N>(k, f, 2) + 5 + ta;
       o.oF4 = FO<N>(k, f, 2) + 9;
-      o.oFW = 72 * k + 6 * ph;
-      const int oFWc = 72 * k + (isv_ ? ph - 6 : 0);
+      o.oFW = kFWS<N> * k + 6 * ph;
+      const int oFWc = kFWS<N> * k + (isv_ ? ph - 6 : 0);
       o.oQL = 36 * k + 6 * (isv_ ? ph - 6 : 0);
       o.oXSp = 12 * k + ph;  // natural order (update_info)
       o.oXSp6 = 12 * k + (ph < 6 ? ph + 6 : ph);

@@ -788,7 +788,9 @@ struct Smem {
   // (N > 32: these three live in the global workspace, Work<N>)
   alignas(16) double Sm[kBig<N> ? 1 : N][GS];  // S_k^{-1} / U_k^{-1} of stage k at SLOT(SIG(k)), row-major (row stride RS)
   double Smpad[2];
-  alignas(16) double FWs[N][kFWS<N>];  // F_k W_k (12x6, row psi at [6 psi]; stage stride kFWS); W_k = B_k' R on rows 6..11
+  // F_k W_k (12x6, row psi at [6 psi]); W_k = B_k' R on rows 6..11: here beyond 32 stages
+  // (stage stride 72), FWs at the end up to 32 stages (stride kFWS = 96)
+  alignas(16) double FWb[kBig<N> ? N : 1][72];
   double QL[kBig<N> ? 1 : N][36];   // B_k F_k W_k = R^{-1} W_k' F_k W_k (6x6)
   union {
     struct {
@@ -817,6 +819,9 @@ struct Smem {
   double dcp[kDC<N> ? 24 * (kRows<N> / 4) : 1];
   alignas(16) double zero[72];  // zeros: masked coefficient reads point here instead of selecting
   int flag[4];
+  // (up to 32 stages) F W at its 96-double stride, last: its round-4 growth leaves every
+  // other array's LDS offset -- and the compiler's register allocation -- as before
+  alignas(16) double FWs[kBig<N> ? 1 : N][kBig<N> ? 2 : kFWS<N>];
 };
 
 // prologue aliases inside GH
@@ -877,10 +882,10 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
   if constexpr (BIG) {
     double* const wk = SOLVE ? a.work + b * Work<N>::SIZE : nullptr;  // (formulation only: unused)
     SmW = (wdd*)(wk + Work<N>::SM);
-    FWW = (lds_d*)&sh.FWs[0][0];  // (Work<N>::FW stays reserved, unused)
+    FWW = (lds_d*)&sh.FWb[0][0];  // (Work<N>::FW stays reserved, unused)
     QLW = (wdd*)(wk + Work<N>::QL);
     if (SOLVE) FRg = (g_d*)(wk + Work<N>::FR + t);
-    zFW = (int)(sh.zero - &sh.FWs[0][0]);
+    zFW = (int)(sh.zero - &sh.FWb[0][0]);
     zQL = Work<N>::ZERO - Work<N>::QL;
     if (SOLVE && t < 72) wk[Work<N>::ZERO + t] = 0.0;
   } else {

@@ -767,6 +767,14 @@ template <int N> constexpr bool kLagOut = N <= 48;
 // instances per CU); not with the deferred check's extra LDS (kDC).
 template <int N>
 constexpr int kFWS = (N <= 32 && !kDC<N>) ? 96 : 72;
+// Up to 16 stages the ADMM loop's exit status goes through LDS (Smem::flag[4]) instead of
+// a register carried across the loop: the N = 16 kernel then spills 27 instead of 43
+// VGPRs (scratch 256 -> 224 B per lane) and its C2 HBM traffic falls 127 -> 88 MB per
+// launch, per-iteration time unchanged (same box, r04u).  At N = 32 the same change made
+// the iteration 1.3 % slower and doubled the traffic through the rho-update path's spills,
+// so the status stays a register there.
+template <int N>
+constexpr bool kXstLds = N <= 16;
 template <int N>
 struct Work {  // offsets (doubles) inside one instance's workspace
   // SM starts two slots in (a pad kept from round 2; the sweep no longer reads it)
@@ -818,7 +826,9 @@ struct Smem {
   double ckx[kDC<N> ? N : 1][12];
   double dcp[kDC<N> ? 24 * (kRows<N> / 4) : 1];
   alignas(16) double zero[72];  // zeros: masked coefficient reads point here instead of selecting
-  int flag[4];
+  // flag[4] (kXstLds): the ADMM loop's exit status, written by thread 0 at the (uniform)
+  // exits and read by every thread after the loop
+  int flag[kXstLds<N> ? 5 : 4];
   // (up to 32 stages) F W at its 96-double stride, last: its round-4 growth leaves every
   // other array's LDS offset -- and the compiler's register allocation -- as before
   alignas(16) double FWs[kBig<N> ? 1 : N][kBig<N> ? 2 : kFWS<N>];
@@ -3031,6 +3041,9 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       // the inner loop iterates until convergence, max_iter or a rho update.
       bool last_checked = false;
       int iter = 1;
+      // the loop's exit status: LDS (kXstLds; read after the loop's closing barrier) or status
+#define MPCQ_SET_XST(v_) do { if constexpr (kXstLds<N>) { if (t == 0) sh.flag[4] = (v_); } else { status = (v_); } } while (0)
+      if constexpr (kXstLds<N>) MPCQ_SET_XST(0);
       int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
       // the bounds are re-derived where used (lo_of / hi_of: a select on the lane's
       // class and its row scaling in the fused path) rather than held in 6 registers
@@ -3047,7 +3060,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
 #ifdef MPCQ_FACTIME
         fac_cycles += __builtin_amdgcn_s_memtime() - ft0_;
 #endif
-        if (!fac_ok) { status = MPCQ_STATUS_FACTOR_FAILED; break; }
+        if (!fac_ok) { MPCQ_SET_XST(MPCQ_STATUS_FACTOR_FAILED); break; }
         STAMP(2);
         bool refactor = false;
         // One ADMM iteration (osqp update_xz_tilde / update_x / update_z / update_y).
@@ -3149,7 +3162,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               int st = 0;
               admm_iter(std::integral_constant<int, 2>{}, ops, dyv, dxf_, dxX_, cvp, &st);
               if (st != 0) {  // the check of the previous iteration ends the solve there
-                status = st;
+                MPCQ_SET_XST(st);
                 --iter;
                 break;
               }
@@ -3186,11 +3199,11 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           infeas_cheap(dyv, dxf_, dxX_, cvp);
           update_info(std::true_type{}, cvp);
           if (inf_need) infeas_products(dxf_, dxX_, cvp);
-          if (!(isfinite(pri_res) && isfinite(dua_res))) { status = MPCQ_STATUS_NONFINITE; break; }
+          if (!(isfinite(pri_res) && isfinite(dua_res))) { MPCQ_SET_XST(MPCQ_STATUS_NONFINITE); break; }
           if (can_check) {  // osqp check_termination
-            if (converged(1.0)) { status = MPCQ_STATUS_SOLVED; break; }
-            if (inf_bits & 1) { status = MPCQ_STATUS_PRIMAL_INFEASIBLE; break; }
-            if (inf_bits & 2) { status = MPCQ_STATUS_DUAL_INFEASIBLE; break; }
+            if (converged(1.0)) { MPCQ_SET_XST(MPCQ_STATUS_SOLVED); break; }
+            if (inf_bits & 1) { MPCQ_SET_XST(MPCQ_STATUS_PRIMAL_INFEASIBLE); break; }
+            if (inf_bits & 2) { MPCQ_SET_XST(MPCQ_STATUS_DUAL_INFEASIBLE); break; }
           }
           if (adapt) {
             double rn = rho_s * sqrt(s_pri / (s_dua + kDivTol));
@@ -3211,6 +3224,11 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         }
         if (!refactor) break;
       }
+      if constexpr (kXstLds<N>) {
+        sync_all();  // thread 0's exit status
+        status = sh.flag[4];
+      }
+#undef MPCQ_SET_XST
       it_done = iter > p.max_iter ? p.max_iter : iter;
       if (status == 0) {
         if (!last_checked) {  // the information of the last (unchecked) iteration

@@ -105,29 +105,60 @@ def parse():
     return ap.parse_args()
 
 
-def load_pmc(tag: str) -> dict:
-    """Per-launch PMC figures (HBM bytes, issued FP64 flops, that run's kernel ms)
-    from the committed rocprofv3 summary profiles/pmc_traffic.json, if any."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+def load_pmc(tag: str, src_sha: str | None = None, path: str | None = None) -> dict:
+    """Per-launch PMC figures (HBM bytes, issued FP64 flops, that run's kernel ms) from the
+    committed rocprofv3 summary profiles/pmc_traffic.json, if any -- only when the entry
+    was profiled on the build that is running: its "engine_src_sha" (the stamp of the
+    profiled libmpcq.so, tools/prof_summary.py) must equal ``src_sha`` (the running
+    library's mpcq_build_info).  Otherwise {"stale": reason} and no figures."""
+    path = path or os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return dict(d.get(tag) or {})
     except (OSError, ValueError):
         return {}
+    e = dict(d.get(tag) or {})
+    if not e:
+        return {}
+    have = e.get("engine_src_sha")
+    if src_sha is None or have != src_sha:
+        return {"stale": f"profiles/pmc_traffic.json[{tag!r}] (tag {e.get('tag')}) was profiled on build "
+                         f"{have or 'unstamped'}, this library is {src_sha or 'unknown'}: figures dropped"}
+    return e
 
 
-def load_traffic(tag: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
-    v = load_pmc(tag).get("bytes_per_launch")
+def lib_sha():
+    """The running libmpcq.so's source stamp (mpcq_build_info), or None."""
+    try:
+        import mpcq
+        return mpcq.build_info().get("src_sha256")
+    except Exception:  # noqa: BLE001 -- no library: no stamp, so no PMC figure is trusted
+        return None
+
+
+def load_traffic(tag: str, src_sha: str | None = None):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any (same build only)."""
+    v = load_pmc(tag, src_sha).get("bytes_per_launch")
     return float(v) if v is not None else None
+
+
+def dist_fields(world: int, backend: str, distributed: bool, torch) -> dict:
+    """How the ranks were spread: the backend, the distinct devices they used (gloo
+    rehearsals share one card round-robin) and whether the line is a rehearsal (ranks
+    sharing devices: not an N-GPU measurement)."""
+    ndev = torch.cuda.device_count()
+    distinct = min(world, ndev) if backend == "gloo" else world
+    return {"backend": backend if distributed else None, "distinct_devices": distinct,
+            "rehearsal": bool(distinct < world)}
 
 
 def _dist_setup():
     """One process per GPU (RANK / LOCAL_RANK / WORLD_SIZE from torch.distributed.run),
     RCCL ("nccl") between them.  MPCQ_DIST_BACKEND=gloo is the rehearsal mode of the
     N > 1 path on a box with fewer GPUs than ranks: ranks share devices round-robin
-    and the collectives (barriers, max-over-ranks, stats) run over gloo on the host."""
+    and the collectives (barriers, max-over-ranks, stats) run over gloo on the host.
+    MPCQ_FORCE_DIST=1 initialises the process group (and so runs every collective of
+    the N > 1 path) at world size 1 too: on a one-GPU box it exercises RCCL itself."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -138,13 +169,21 @@ def _dist_setup():
         raise ValueError(f"MPCQ_DIST_BACKEND={backend!r}: 'nccl' (RCCL) or 'gloo'")
     if backend == "gloo":
         local = local % max(torch.cuda.device_count(), 1)
-    if world > 1:
+    if world > 1 or os.environ.get("MPCQ_FORCE_DIST") == "1":
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            from mpcq import launch
+            os.environ["MASTER_PORT"] = str(launch.free_port())
         torch.cuda.set_device(local)
-        dist.init_process_group(backend, init_method="env://")
+        dist.init_process_group(backend, init_method="env://", rank=rank, world_size=world)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     coll = dev if backend == "nccl" else torch.device("cpu")  # where collective tensors live
     return torch, dist, world, rank, local, dev, coll
+
+
+def _distributed(dist) -> bool:
+    return dist.is_available() and dist.is_initialized()
 
 
 def _timed(torch, dist, dev, coll, world, stream, step, steps, warmup):
@@ -155,7 +194,7 @@ def _timed(torch, dist, dev, coll, world, stream, step, steps, warmup):
     for i in range(warmup):
         step(i)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if _distributed(dist):
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -166,7 +205,7 @@ def _timed(torch, dist, dev, coll, world, stream, step, steps, warmup):
         step(warmup + i)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if _distributed(dist):
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
@@ -215,10 +254,11 @@ def main_plan(args):
                "config": {"workload": f"planner tick, {per} robots per GPU, N={N}", "horizon": N,
                           "parallelism": f"shard{world}"},
                "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                            "frac": ach / PEAK_HBM_GBS, "traffic": load_traffic(f"plan_N{N}_B{per}"),
+                            "frac": ach / PEAK_HBM_GBS, "traffic": load_traffic(f"plan_N{N}_B{per}", lib_sha()),
                             "note": f"algorithmic {model.planner_bytes_per_instance(N)} B/robot x {per} robots "
                                     "per launch / HIP-event launch time"},
-               "kernel_ms_per_launch": ms, "ok_fraction": ok / per}
+               "kernel_ms_per_launch": ms, "ok_fraction": ok / per,
+               "dist": dist_fields(world, os.environ.get("MPCQ_DIST_BACKEND", "nccl"), _distributed(dist), torch)}
         if world == 1 and args.cpu_sample > 0:
             from oracle import oracle as O
             O.build()
@@ -236,7 +276,7 @@ def main_plan(args):
                                              f"1 thread, {tc:.1f} s"}
         print(json.dumps(out), flush=True)
     eng.close()
-    if world > 1:
+    if _distributed(dist):
         dist.destroy_process_group()
 
 
@@ -283,6 +323,7 @@ def main_tick(args):
                                     "taken as 0 -- a lower bound) / its HIP-event time"},
                "kernel_ms": {"step": ms, "planner_last_tick": plan_ms, "solve_last_tick": solve_ms},
                "solved_fraction": float(np.isin(st, (1, 2)).mean()),
+               "dist": dist_fields(world, os.environ.get("MPCQ_DIST_BACKEND", "nccl"), _distributed(dist), torch),
                "iters_warm": {"median": float(np.median(it)), "p90": float(np.percentile(it, 90)),
                               "max": int(it.max())}}
         if world == 1 and args.cpu_sample > 0:
@@ -303,7 +344,7 @@ def main_tick(args):
         print(json.dumps(out), flush=True)
     sess.close()
     eng.close()
-    if world > 1:
+    if _distributed(dist):
         dist.destroy_process_group()
 
 
@@ -443,13 +484,13 @@ def main():
 
         def step():
             launch()
-            if gather and world > 1:
+            if gather and _distributed(dist):
                 shard.gather_rows(dist, f0_d if coll.type == "cuda" else f0_d.cpu(), total, world, rank)
 
         for _ in range(warmup):
             step()
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if _distributed(dist):
             dist.barrier()
         torch.cuda.synchronize(dev)
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(timed_steps + 1)]
@@ -459,7 +500,7 @@ def main():
             step()
             evs[i + 1].record(stream)
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if _distributed(dist):
             dist.barrier()
         torch.cuda.synchronize(dev)
         wall = time.perf_counter() - t0
@@ -505,7 +546,7 @@ def main():
     fl, fl_dense = work(head), work(head, structured=False)
     by = model.bytes_per_instance(N) * per
     stats = torch.tensor([solved, per, fl, by, kern_ms], dtype=torch.float64, device=coll)
-    if world > 1:
+    if _distributed(dist):
         allst = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(allst, stats)
         allst = torch.stack(allst).cpu().numpy()
@@ -526,7 +567,8 @@ def main():
         value = float(allst[:, 0].sum()) * args.steps / wall_max
         fl0, by0 = float(allst[0, 2]), float(allst[0, 3])
         tag = f"{args.config}_N{N}_B{per}" + ("_polish" if pol else "")
-        pmc = load_pmc(tag)
+        src_sha = lib_sha()
+        pmc = load_pmc(tag, src_sha)
         roof = {"bound": "valu_fp64", "achieved": fl0 / (kern_ms * 1e-3) / 1e12, "peak": PEAK_FP64_TFLOPS,
                 "unit": "TFLOP/s", "frac": None, "traffic": pmc.get("bytes_per_launch"),
                 "achieved_dense_model": fl_dense / (kern_ms * 1e-3) / 1e12,
@@ -567,6 +609,8 @@ def main():
                        "parallelism": f"shard{world}" + ("+gather" if args.gather else "")},
             "roofline": roof,
             "roofline_hbm": roof_hbm,
+            "build": {"engine_src_sha": src_sha, "pmc_tag": pmc.get("tag"), "pmc_stale": pmc.get("stale")},
+            "dist": dist_fields(world, os.environ.get("MPCQ_DIST_BACKEND", "nccl"), _distributed(dist), torch),
             "kernel_ms_per_launch": kern_ms,
             "kernel_ms_launches": {"median": float(np.median(launch_ms)), "min": float(launch_ms.min()),
                                    "max": float(launch_ms.max())},
@@ -691,7 +735,7 @@ def main():
         out["parity"] = par
         print(json.dumps(out), flush=True)
 
-    if world > 1:
+    if _distributed(dist):
         dist.destroy_process_group()
 
 

@@ -127,6 +127,10 @@ int mpcq_pattern(int n_steps, int32_t* indptr, int32_t* indices);
 /* Horizons compiled into the HIP engine (writes up to cap values). */
 int mpcq_supported_horizons(int32_t* out, int cap);
 const char* mpcq_last_error(void);
+/* Build stamp of this library (no reference counterpart: provenance for profiles):
+ * "src_sha256=<first 16 hex of sha256 over the csrc .hip files in name order> arch=gfx950".
+ * bench.py drops a committed PMC figure whose stamp differs from the running library's. */
+const char* mpcq_build_info(void);
 
 /* ---- context --------------------------------------------------------------
  * Replaces MPC.MPC(dt, n_steps, T_gait) (MPC.py:22-82) + osqp.OSQP() (MPC.py:73).

@@ -461,104 +461,6 @@ __device__ __forceinline__ void schur_cols(double (&Ro)[12], const double (&G)[1
                                            const double (&c6)[6], std::integer_sequence<int, C...>) {
   (schur_col<C, FOLD>(Ro, G, ca, c6), ...);
 }
-// i0 + sum_m c_m(lane J) g_m: twelve registers broadcast from one lane J of the row, the
-// broadcast folded into v_fmac_f64_dpp (as one asm block the compiler cannot hoist the
-// 144 broadcasts of a dense Schur update ahead of their products and spill them)
-#define MPCQ_BDOT_LANE(J)                                                                    \
-  asm("s_nop 1\n\t" \
-      "v_fmac_f64_dpp %0, %1, %13 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %2, %14 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %3, %15 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %4, %16 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %5, %17 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %6, %18 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %7, %19 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %8, %20 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %9, %21 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %10, %22 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %11, %23 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %12, %24 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" \
-      : "+v"(a0)                                                                             \
-      : "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]),   \
-        "v"(c[8]), "v"(c[9]), "v"(c[10]), "v"(c[11]), "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]),  \
-        "v"(g[4]), "v"(g[5]), "v"(g[6]), "v"(g[7]), "v"(g[8]), "v"(g[9]), "v"(g[10]), "v"(g[11]))
-template <int J>
-__device__ __forceinline__ double bdot_lane(const double (&c)[12], const double (&g)[12], double i0) {
-  double a0 = i0;
-  if constexpr (J == 0) MPCQ_BDOT_LANE(0);
-  else if constexpr (J == 1) MPCQ_BDOT_LANE(1);
-  else if constexpr (J == 2) MPCQ_BDOT_LANE(2);
-  else if constexpr (J == 4) MPCQ_BDOT_LANE(4);
-  else if constexpr (J == 5) MPCQ_BDOT_LANE(5);
-  else if constexpr (J == 6) MPCQ_BDOT_LANE(6);
-  else if constexpr (J == 8) MPCQ_BDOT_LANE(8);
-  else if constexpr (J == 9) MPCQ_BDOT_LANE(9);
-  else if constexpr (J == 10) MPCQ_BDOT_LANE(10);
-  else if constexpr (J == 12) MPCQ_BDOT_LANE(12);
-  else if constexpr (J == 13) MPCQ_BDOT_LANE(13);
-  else if constexpr (J == 14) MPCQ_BDOT_LANE(14);
-  else static_assert(J < 0, "a column lane LN(i)");
-  return a0;
-}
-#undef MPCQ_BDOT_LANE
-// The sparse Schur column of schur_col with its seven broadcasts folded into
-// v_fmac_f64_dpp (the cyclic reduction's factorisation runs two of these updates back
-// to back; as separate moves the compiler hoisted all 168 broadcasts and spilled them)
-#define MPCQ_BDOT7_LANE(J)                                                                   \
-  asm("s_nop 1\n\t" \
-      "v_fmac_f64_dpp %0, %1, %8 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %2, %9 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %3, %10 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %4, %11 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %5, %12 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %6, %13 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
-      "v_fmac_f64_dpp %0, %7, %14 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" \
-      : "+v"(a0)                                                                             \
-      : "v"(ca), "v"(c6[0]), "v"(c6[1]), "v"(c6[2]), "v"(c6[3]), "v"(c6[4]), "v"(c6[5]), "v"(ga),  \
-        "v"(g6[0]), "v"(g6[1]), "v"(g6[2]), "v"(g6[3]), "v"(g6[4]), "v"(g6[5]))
-template <int J>
-__device__ __forceinline__ double bdot7_lane(double ca, const double (&c6)[6], double ga, const double (&g6)[6],
-                                             double i0) {
-  double a0 = i0;
-  if constexpr (J == 0) MPCQ_BDOT7_LANE(0);
-  else if constexpr (J == 1) MPCQ_BDOT7_LANE(1);
-  else if constexpr (J == 2) MPCQ_BDOT7_LANE(2);
-  else if constexpr (J == 4) MPCQ_BDOT7_LANE(4);
-  else if constexpr (J == 5) MPCQ_BDOT7_LANE(5);
-  else if constexpr (J == 6) MPCQ_BDOT7_LANE(6);
-  else if constexpr (J == 8) MPCQ_BDOT7_LANE(8);
-  else if constexpr (J == 9) MPCQ_BDOT7_LANE(9);
-  else if constexpr (J == 10) MPCQ_BDOT7_LANE(10);
-  else if constexpr (J == 12) MPCQ_BDOT7_LANE(12);
-  else if constexpr (J == 13) MPCQ_BDOT7_LANE(13);
-  else if constexpr (J == 14) MPCQ_BDOT7_LANE(14);
-  else static_assert(J < 0, "a column lane LN(i)");
-  return a0;
-}
-#undef MPCQ_BDOT7_LANE
-template <int CI>
-__device__ __forceinline__ void schur_col_a(double (&Ro)[12], const double (&G)[12], double ca,
-                                            const double (&c6)[6]) {
-  const double g6[6] = {G[6], G[7], G[8], G[9], G[10], G[11]};
-  Ro[CI] -= bdot7_lane<LN(CI)>(ca, c6, G[CI < 6 ? CI : CI - 6], g6, 0.0);
-}
-template <int... C>
-__device__ __forceinline__ void schur_cols_a(double (&Ro)[12], const double (&G)[12], double ca,
-                                             const double (&c6)[6], std::integer_sequence<int, C...>) {
-  (schur_col_a<C>(Ro, G, ca, c6), ...);
-}
-// Ro -= G C' for a dense 12x12 coupling C held one row per column lane (the reduced
-// system of the cyclic reduction): column CI takes row CI of C from lane LN(CI)
-template <int CI>
-__device__ __forceinline__ void schur_dcol(double (&Ro)[12], const double (&G)[12], const double (&C)[12]) {
-  Ro[CI] -= bdot_lane<LN(CI)>(C, G, 0.0);
-}
-template <int... C>
-__device__ __forceinline__ void schur_dcols(double (&Ro)[12], const double (&G)[12], const double (&Cm)[12],
-                                            std::integer_sequence<int, C...>) {
-  (schur_dcol<C>(Ro, G, Cm), ...);
-}
-
 // ---------------------------------------------------------------------------
 // Formulation pieces (restating MPC.py; oracle/mpcq_oracle.c is the CPU twin)
 
@@ -652,73 +554,10 @@ constexpr int kSlotPad = 2;
 template <int N>
 __host__ __device__ constexpr int SLOT(int q) { return GS * q + (q > N / 2 ? kSlotPad<N> : 0); }
 
-// One level of block cyclic reduction of the state system (round 4).  The odd
-// stages are eliminated stage-parallel: with T_{k,k-1} = L_k, T_{kk} = D_k,
-//   x_o = D_o^{-1} (b_o - L_o x_{o-1} - L_{o+1}' x_{o+1})        (o odd)
-// leaves a block-tridiagonal system on the even stages e = 2j (NS = N/2 of them)
-//   D'_j = D_e - L_e D_{e-1}^{-1} L_e' - L_{e+1}' D_{e+1}^{-1} L_{e+1}
-//   L''_j = -L_e D_{e-1}^{-1} L_{e-1}                              (T'_{j,j-1})
-//   b'_j = b_e - L_e D_{e-1}^{-1} b_{e-1} - L_{e+1}' D_{e+1}^{-1} b_{e+1}
-// which the two-ended sweep solves in N/2 + 1 dependent steps instead of N + 1:
-// per iteration the serial chain halves, for two stage-parallel phases (the
-// reduction of b and the back-substitution of the odd stages).
-// Measured and NOT the default (round 4, profiles/r04b_*, r04c_*): the factorisation
-// is faster (N = 16 87 k vs 103 k cycles, N = 32 109 k vs 144 k) and the sweep
-// shorter, but each of the two phases costs ~1450 cycles per iteration (~130
-// instructions per wave with four LDS round trips, plus a barrier) against ~200 per
-// sweep step saved: 1.81 -> 2.55 us per iteration alone at N = 16, 3.15 -> 4.09 at
-// N = 32; C2 126 k -> 88 k QP/s.  Lean phases would need the products L D^{-1}
-// precomputed per lane (24 doubles per lane), which neither LDS nor the VGPR budget
-// holds.  Build with -DMPCQ_CR to get it (parity-green on the GPU suite's CR horizons).
-#ifdef MPCQ_CR
-template <int N>
-constexpr bool kCR = N % 4 == 0 && N >= 8 && N <= 32;
-#else
-template <int N>
-constexpr bool kCR = false;
-#endif
-// The deferred termination check (round 4).  A check that is not an adaptive-rho
-// step and not the last iteration runs inside the next iteration ("the carrier"): the
-// checked iteration publishes its states / duals and the cheap infeasibility partials
-// (no barrier), the carrier's own right-hand-side barrier publishes them, every wave
-// but the sweep wave forms its stages' residual terms while wave 0 runs the sweep
-// (wave 0 after it), and after the force-recovery barrier every lane combines them:
-// a converged (or infeasible) check stops the solve before the carrier's z / y / x
-// update, so the result is the checked iteration's -- the same decisions, iteration
-// counts and bits as the blocking check, which stays for the adaptive-rho steps, the
-// last iteration and beyond 32 stages.
-// Measured and NOT the default (round 4, profiles/r04d_*): the GPU suite passes on it
-// (73/73, same statuses / iterations), but a check costs 4.00 us on the critical path
-// against 3.43 blocking (tools/checkcost.py, N = 16, interval 25), and the unchecked
-// iteration 1.675 vs 1.657 us: wave 0 still forms its own four stages' terms (~400
-// instructions, the bulk of the check) after its sweep, now behind an exposed
-// private-memory load of the constant block; moving them to another wave needs wave 0's
-// x / z / y in LDS (352 doubles at N = 16) where 344 are left.  Build with -DMPCQ_DC.
-#ifdef MPCQ_DC
-template <int N>
-constexpr bool kDC = N <= 32 && !kCR<N>;
-#else
-template <int N>
-constexpr bool kDC = false;
-#endif
-template <int N>
-struct CRL {  // offsets (doubles) of the reduction's arrays (kCR<N>)
-  static constexpr int NS = N / 2;
-  // in GH, past the reduced sweep's slots (SLOT<NS> reaches GS NS + 2): row i of
-  // D_o^{-1} of odd stage o at DI + GS (o >> 1) + RS i
-  static constexpr int DI = GS * NS + 2;
-  // in Sm, past the reduced S^{-1} slots: L_k compact, 48 doubles per stage: a[6]
-  // (L[i][i], i < 6), t[6] (L[i][6+i], i < 6), V[6][6] (L[6+i][6+j]); the other
-  // entries are structurally zero (Ctop)
-  static constexpr int LS = GS * NS + 2;
-  // in u.it.xs: the reduced sweep's states at SIGX<NS> slots (NS + 1 slots), then
-  // the odd stages' states, X of odd stage o at XO + 12 (o >> 1)
-  static constexpr int XO = 12 * (NS + 1);
-};
-static_assert(CRL<32>::DI + GS * 16 == GS * 32 + 2 && CRL<32>::LS + 48 * 32 <= GS * 32 + 2 &&
-                  CRL<32>::XO + 12 * 16 == 12 * 33,
-              "the reduction's arrays fit GH / Sm / xs");
-
+// Rejected round-4 solve variants (block cyclic reduction of the state system; the
+// termination check deferred into the next iteration) were measured slower and removed
+// in round 5; their code is kept as a patch, tools/attic/engine_cr_dc_round4.patch, and
+// their measurements in DESIGN.md section 8 (round 4) items 3-4.
 // Horizons beyond 32 stages do not fit a CU's LDS (N = 48: 236 KB): S^{-1}, F W and
 // R^{-1} Q move to a per-instance global workspace (LaunchArgs::work, work_doubles(N)
 // doubles per instance, L2-resident), the rest stays in LDS (N = 48: 140 KB).
@@ -764,9 +603,9 @@ template <int N> constexpr bool kLagOut = N <= 48;
 // ph 6/7/8 of the next in the same banks (2-way conflicts); at a 96-double stride (256 B
 // x 3, stages 0 mod 16 units apart) the twelve rows of each group land in distinct banks.
 // Up to 32 stages, where the LDS has the 24 N doubles (N = 16: 80,048 B, still two
-// instances per CU); not with the deferred check's extra LDS (kDC).
+// instances per CU).
 template <int N>
-constexpr int kFWS = (N <= 32 && !kDC<N>) ? 96 : 72;
+constexpr int kFWS = N <= 32 ? 96 : 72;
 // Up to 16 stages the ADMM loop's exit status goes through LDS (Smem::flag[4]) instead of
 // a register carried across the loop: the N = 16 kernel then spills 27 instead of 43
 // VGPRs (scratch 256 -> 224 B per lane) and its C2 HBM traffic falls 127 -> 88 MB per
@@ -814,17 +653,15 @@ struct Smem {
     struct {
       alignas(16) double St[144];  // sweep hand-offs of the factorisation (16-B aligned: the
       alignas(16) double Sb[144];  // couplings read them as column pairs)
-      double Lm[144];           // (kCR) the reduced meeting row's lower coupling
     } fa;
   } u;
   // per-wave partial reductions (32 per wave); during the sweeps the sink of lanes
   // whose store is void (lane (t & 31) + 12 j, j <= N/2 + 1)
   double red[(8 * kRows<N> + 32 > 12 * (N / 2 + 2) + 32) ? 8 * kRows<N> + 32 : 12 * (N / 2 + 2) + 32];
   double dump[64];          // sink of predicated stores (never read): lane & 63
-  // (kDC) the deferred check: the checked iteration's states X_{k+1} (the duals go to
-  // u.it.nb), and per wave 16 residual maxima + the cheap infeasibility partials
-  double ckx[kDC<N> ? N : 1][12];
-  double dcp[kDC<N> ? 24 * (kRows<N> / 4) : 1];
+  // (13 unused doubles: where round 4's deferred-check arrays sat; they keep every later
+  // array's LDS offset, and with it the compiler's register allocation, as measured)
+  double pad13_[13];
   alignas(16) double zero[72];  // zeros: masked coefficient reads point here instead of selecting
   // flag[4] (kXstLds): the ADMM loop's exit status, written by thread 0 at the (uniform)
   // exits and read by every thread after the loop
@@ -869,7 +706,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
   if ((int64_t)blockIdx.x >= a.batch) return;
   const int64_t b = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;  // the instance
   STAMP_DECL
-  constexpr bool BIG = kBig<N>, ABG = kAbG<N>, CR = kCR<N>;
+  constexpr bool BIG = kBig<N>, ABG = kAbG<N>;
   // the scaled constraint values: LDS, or (N > 49) this instance's workspace (the
   // formulation-only launch builds them straight into its Ax output)
   using acd = std::conditional_t<ABG, g_cd, lds_cd>;
@@ -1432,178 +1269,6 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         }
         schur_cols<!kBig<N>>(Ro, G, ca, c6, std::make_integer_sequence<int, 12>{});
       };
-      if constexpr (CR) {
-        // ---- cyclic reduction (kCR): D_o^{-1} of the odd stages, the reduced system
-        // on the even stages, then its two-ended factorisation (NS stages, dense
-        // couplings).  The stage-keyed scratch is dead once every lane holds its
-        // D / L rows (the barrier below); D^{-1} then reuses those GH slots.
-        constexpr int NS = CRL<N>::NS, MIDS = NS / 2;
-        const bool odd = (k & 1) != 0;
-        sync_all();
-        if (cl) {  // own row of L_k, compact (stage 0 has no L: zeros)
-          double* const q = &sh.Sm[0][0] + CRL<N>::LS + 48 * k;
-          if (ph < 6) {
-            q[ph] = k ? cta : 0.0;
-            q[6 + ph] = k ? ct6[ph] : 0.0;
-          } else {
-#pragma unroll
-            for (int j = 0; j < 6; ++j) q[12 + 6 * (ph - 6) + j] = k ? ct6[j] : 0.0;
-          }
-        }
-        if (odd) {
-          double Ro[12];
-#pragma unroll
-          for (int ci = 0; ci < 12; ++ci) Ro[ci] = Dr0[ci];
-          gj12<!kBig<N>>(Ro, ph, ok);
-          if (cl) {
-            double* const q = gh0 + CRL<N>::DI + GS * (k >> 1) + RS * ph;
-#pragma unroll
-            for (int ci = 0; ci < 12; ++ci) q[ci] = Ro[ci];
-          }
-        }
-        sync_all();
-        // Even stages: row ph of D'_j and of the reduced coupling the factorisation step of
-        // reduced stage j = k / 2 takes -- L''_j (lt: top rows and the meeting) or
-        // L''_{j+1}' (lb: bottom rows and the meeting) -- staged in LDS for the serial
-        // steps (held in registers across them they spilled): D' in GH slot SIG<NS>(j), the
-        // coupling row in Sm slot SIG<NS>(j) (each overwritten by its own row's G / S^{-1}
-        // at its step, after the read), the meeting row's lb past St / Sb in u.fa.
-        double* const lbm = sh.u.fa.Lm;  // the meeting row's lb (12 x 12)
-        // Ro -= (C S^{-1}) C' for the compact row (ca, c6) of a sparse coupling C; G = C S^{-1}
-        auto couple_sp = [&](double ca, const double (&c6)[6], const double* Sp, double (&Ro)[12],
-                             double (&G)[12]) __attribute__((always_inline)) {
-          const int ar = ph < 6 ? ph : ph - 6;
-#pragma unroll
-          for (int ci = 0; ci < 12; ++ci) {
-            double sv[7];
-            sv[0] = Sp[12 * ar + ci];
-#pragma unroll
-            for (int j = 0; j < 6; ++j) sv[1 + j] = Sp[12 * (6 + j) + ci];
-            double gv = ca * sv[0];
-#pragma unroll
-            for (int j = 0; j < 6; ++j) gv = fma(c6[j], sv[1 + j], gv);
-            G[ci] = gv;
-            asm volatile("" ::: "memory");
-          }
-          schur_cols_a(Ro, G, ca, c6, std::make_integer_sequence<int, 12>{});
-        };
-        if (!odd) {
-          const int jr = k >> 1;
-          const double* const Lsb = &sh.Sm[0][0] + CRL<N>::LS;
-          double* const lslot = &sh.Sm[0][0] + SLOT<NS>(SIG<NS>(jr)) + RS * ph;
-          double Dp[12], G[12];
-#pragma unroll
-          for (int ci = 0; ci < 12; ++ci) Dp[ci] = Dr0[ci];
-          if (k >= 1) {  // - L_k D_{k-1}^{-1} L_k'
-            couple_sp(cta, ct6, gh0 + CRL<N>::DI + GS * ((k - 1) >> 1), Dp, G);
-            if (k >= 2 && jr <= MIDS) {  // lt = -(L_k D_{k-1}^{-1}) L_{k-1}, row ph
-              const double* const q = Lsb + 48 * (k - 1);
-              double lt[12];
-#pragma unroll
-              for (int c_ = 0; c_ < 6; ++c_) lt[c_] = -(G[c_] * q[c_]);
-#pragma unroll
-              for (int jj = 0; jj < 6; ++jj) {
-                double v = G[jj] * q[6 + jj];
-#pragma unroll
-                for (int m_ = 0; m_ < 6; ++m_) v = fma(G[6 + m_], q[12 + 6 * m_ + jj], v);
-                lt[6 + jj] = -v;
-              }
-              if (cl) {
-#pragma unroll
-                for (int ci = 0; ci < 12; ++ci) lslot[ci] = lt[ci];
-              }
-            }
-          }
-          // - L_{k+1}' D_{k+1}^{-1} L_{k+1} (k + 1 <= N - 1: N is even)
-          couple_sp(cba, cb6, gh0 + CRL<N>::DI + GS * (k >> 1), Dp, G);
-          if (k + 2 <= N - 1 && jr >= MIDS) {  // lb = -(L_{k+1}' D_{k+1}^{-1}) L_{k+2}', row ph
-            const double* const q = Lsb + 48 * (k + 2);
-            double lb[12];
-#pragma unroll
-            for (int c_ = 0; c_ < 6; ++c_) lb[c_] = -(G[c_] * q[c_] + G[6 + c_] * q[6 + c_]);
-#pragma unroll
-            for (int jj = 0; jj < 6; ++jj) {
-              double v = G[6] * q[12 + 6 * jj];
-#pragma unroll
-              for (int m_ = 1; m_ < 6; ++m_) v = fma(G[6 + m_], q[12 + 6 * jj + m_], v);
-              lb[6 + jj] = -v;
-            }
-            if (cl) {
-              double* const d = jr == MIDS ? lbm + 12 * ph : lslot;
-#pragma unroll
-              for (int ci = 0; ci < 12; ++ci) d[ci] = lb[ci];
-            }
-          }
-          if (cl) {
-            double* const d = gh0 + SLOT<NS>(SIG<NS>(jr)) + RS * ph;
-#pragma unroll
-            for (int ci = 0; ci < 12; ++ci) d[ci] = Dp[ci];
-          }
-        }
-        sync_all();
-        // one coupling of the reduced factorisation: Ro -= (C S^{-1}) C' for the dense
-        // row C of this lane, S^{-1} (St / Sb) row by row; -G stored at Gd
-        auto couple_dn = [&](const double (&C)[12], const double* Sp, double* Gd, double (&Ro)[12])
-            __attribute__((always_inline)) {
-          double G[12];
-#pragma unroll
-          for (int ci = 0; ci < 12; ++ci) G[ci] = 0.0;
-#pragma unroll
-          for (int m_ = 0; m_ < 12; ++m_) {
-            double sr[12];
-#pragma unroll
-            for (int ci = 0; ci < 12; ++ci) sr[ci] = Sp[12 * m_ + ci];
-#pragma unroll
-            for (int ci = 0; ci < 12; ++ci) G[ci] = fma(C[m_], sr[ci], G[ci]);
-            asm volatile("" ::: "memory");
-          }
-          wave_sync();  // the row's reads of the slot G goes to are done
-          if (cl) {
-#pragma unroll
-            for (int ci = 0; ci < 12; ++ci) Gd[ci] = -G[ci];
-          }
-          schur_dcols(Ro, G, C, std::make_integer_sequence<int, 12>{});
-        };
-        // the reduced system's two-ended factorisation (as below, on NS stages): step
-        // jj < MIDS: top reduced stage jj and bottom NS-1-jj > MIDS; step MIDS: the meeting
-#pragma nounroll
-        for (int jj = 0; jj <= MIDS; ++jj) {
-          launder();
-          const int j = k >> 1;
-          const bool ev = (k & 1) == 0, mid = jj == MIDS;
-          const bool top = ev && !mid && j == jj, bot = ev && !mid && j == NS - 1 - jj && j > MIDS,
-                     mrow = ev && mid && j == MIDS;
-          if (top || bot || mrow) {
-            const bool useT = (top && j > 0) || mrow, useB = (bot && j < NS - 1) || mrow;
-            double* const gs = gh0 + SLOT<NS>(SIG<NS>(j)) + RS * ph;
-            const double* const ls = &sh.Sm[0][0] + SLOT<NS>(SIG<NS>(j)) + RS * ph;
-            double Ro[12], C[12];
-#pragma unroll
-            for (int ci = 0; ci < 12; ++ci) { Ro[ci] = gs[ci]; C[ci] = ls[ci]; }
-            if (useT) couple_dn(C, St, gs, Ro);
-            if (useB) {
-              if (mrow) {
-#pragma unroll
-                for (int ci = 0; ci < 12; ++ci) C[ci] = lbm[12 * ph + ci];
-              }
-              couple_dn(C, Sb, gh0 + SLOT<NS>(SIG<NS>(j + 1)) + RS * ph, Ro);
-            }
-            gj12<!kBig<N>>(Ro, ph, ok);
-            wave_sync();  // the row's reads of its coupling slot are done
-            if (cl) {
-#pragma unroll
-              for (int ci = 0; ci < 12; ++ci) SmW[SLOT<NS>(SIG<NS>(j)) + RS * ph + ci] = Ro[ci];
-            }
-            wave_sync();  // the previous inverse has been consumed by this row
-            if (cl) {
-              double* dst = mrow ? &sh.GH[0][RS * ph] : (bot ? Sb : St) + 12 * ph;
-#pragma unroll
-              for (int ci = 0; ci < 12; ++ci) dst[ci] = Ro[ci];
-            }
-          }
-          sync_all();
-        }
-      } else {
       // Step j < MID: top row k = j and bottom row k = N-1-j > MID in parallel; step
       // MID: the meeting row (both couplings).  M^{-1} -> GH[0].
 #pragma nounroll
@@ -1632,7 +1297,6 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         }
         sync_all();
       }
-      }  // !CR
       STAMP(14);
       // a non-positive pivot anywhere fails the whole instance (uniform result)
       if (!ok) atomicOr(&sh.flag[2], 1);
@@ -1689,12 +1353,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       o.oXSp = 12 * k + ph;  // natural order (update_info)
       o.oXSp6 = 12 * k + (ph < 6 ? ph + 6 : ph);
       // the sweep's states in its slots (SIGX): own X_{k+1}, the previous stage's X_k
-      // (cyclic reduction: the even stages' states in the reduced sweep's slots, the
-      // odd ones after them)
-      auto xsl = [](int kk) __attribute__((always_inline)) -> int {
-        if constexpr (kCR<N>) return (kk & 1) ? CRL<N>::XO + 12 * (kk >> 1) : 12 * SIGX<CRL<N>::NS>((kk >> 1) + 1);
-        else return 12 * SIGX<N>(kk + 1);
-      };
+      auto xsl = [](int kk) __attribute__((always_inline)) -> int { return 12 * SIGX<N>(kk + 1); };
       o.rXS = xsl(k) + ph;
       o.rXSpm = hp_ ? xsl(k - 1) + ph : zXS;
       o.rXSp6m = hp_ ? xsl(k - 1) + (ph < 6 ? ph + 6 : ph) : zXS;
@@ -2158,52 +1817,6 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       STAMP(8);
       info_combine(inf_tag, cv, sh.red, 32);
       sync_all();
-    };
-    // ---- the deferred check (kDC) -----------------------------------------------
-    // the checked iteration's deltas x / y (and dyp) for the products pass, private
-    double dc_mem_[kDC<N> ? 5 : 1];
-    auto dc_ptr = [&]() __attribute__((always_inline)) -> pdbl* {
-      pdbl* q = (pdbl*)&dc_mem_[0];
-      asm volatile("" : "+v"(q));
-      return q;
-    };
-    // at the checked iteration (after its update): publish X / y for the carrier's
-    // residual terms and the cheap infeasibility partials, keep the deltas; no barrier
-    // (the carrier's right-hand-side barrier publishes it all)
-    auto dc_publish = [&](const double (&dy)[3], double dxf, double dxX, const double (&cv)[CK_COUNT])
-        __attribute__((always_inline)) {
-      if constexpr (kDC<N>) {
-        cheap_partials(dy, dxf, dxX, cv, sh.dcp, 24);
-        if (cl) { sh.ckx[k][ph] = xX; sh.u.it.nb[k][ph] = y[0]; }
-        pdbl* const q = dc_ptr();
-        q[0] = dxf; q[1] = dxX; q[2] = dyp[0]; q[3] = dyp[1]; q[4] = dyp[2];
-      }
-    };
-    // in the carrier, after its sweep (waves 1.. while wave 0 sweeps): the residual terms
-    // of the checked iteration, whose x / z / y the carrier has not updated yet
-    auto dc_terms = [&](const double (&cv)[CK_COUNT]) __attribute__((always_inline)) {
-      if constexpr (kDC<N>) {
-        launder_p();
-        info_terms(cv, (lds_cd*)&sh.ckx[0][0], &sh.u.it.nb[0][0], sh.dcp, 24);
-      }
-    };
-    // the products pass of the infeasibility tests for a deferred check (inf_need != 0):
-    // the deltas published where infeas_products reads them (the carrier's sweep is done
-    // with na / nb), the cheap maxima ndy / ndx copied to red, then infeas_products
-    auto dc_products = [&](const double (&cv)[CK_COUNT]) __attribute__((always_inline)) {
-      if constexpr (kDC<N>) {
-        MPCQ_CHECK_IDS();
-        pdbl* const q = dc_ptr();
-        const double dxf = q[0], dxX = q[1];
-        dyp[0] = q[2]; dyp[1] = q[3]; dyp[2] = q[4];
-        if (cl) {
-          sh.u.it.na[k][ph] = dxX;
-          sh.u.it.nb[k][ph] = dyp[0];
-        }
-        if (lane == 0 || lane == 4) sh.red[32 * wv + 16 + (lane >> 1)] = sh.dcp[24 * wv + 16 + (lane >> 1)];
-        sync_all();
-        infeas_products(dxf, dxX, cv);
-      }
     };
     auto converged = [&](double fac) __attribute__((always_inline)) {
       return pri_res < fac * eps_pri && dua_res < fac * eps_dua;
@@ -2730,7 +2343,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
                                      : (cr == 0 ? (j > 2 ? j : 2) : (j < BOT + 1 ? j : BOT + 1));
             return Mb + GS * jj;
           };
-          if constexpr (!CR) STAMP(15);  // (diagnostic builds: as in ph_sweep_split)
+          STAMP(15);  // (diagnostic builds: as in ph_sweep_split)
           if (t < 64) row12(rowp(1));
           sync_all();
           STAMP(ST);
@@ -2863,122 +2476,10 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           wave_sync();
           }  // MPCQ_REP_SWEEP
       };
-      // ---- the cyclic reduction's stage-parallel phases (kCR) ------------------
-      // L_kk on the compact store, per lane: (L v)[ph] = cA v[ph] + cT v[ph +- 6] +
-      // sum_j cV[j] v[6 + j], v(lane LN(i)) = v[i]; the structural zeros read sh.zero.
-      // Row ph of L_kk:
-      auto cr_lrow = [&](int kk, double& cA, double& cT, double (&cV)[6]) __attribute__((always_inline)) {
-        lds_cd* const q = (lds_cd*)&sh.Sm[0][0] + CRL<N>::LS + 48 * kk;
-        lds_cd* const zz = (lds_cd*)sh.zero;
-        const bool lo = ph < 6;
-        cA = *(lo ? q + ph : zz);
-        cT = *(lo ? q + 6 + ph : zz);
-        lds_cd* const qv = lo ? zz : q + 12 + 6 * (ph - 6);
-#pragma unroll
-        for (int j = 0; j < 6; ++j) cV[j] = qv[j];
-      };
-      // column ph of L_kk (a row of L_kk')
-      auto cr_lcol = [&](int kk, double& cA, double& cT, double (&cV)[6]) __attribute__((always_inline)) {
-        lds_cd* const q = (lds_cd*)&sh.Sm[0][0] + CRL<N>::LS + 48 * kk;
-        lds_cd* const zz = (lds_cd*)sh.zero;
-        const bool lo = ph < 6;
-        cA = *(lo ? q + ph : zz);
-        cT = *(lo ? zz : q + ph);  // t[ph - 6] at q + 6 + (ph - 6)
-        lds_cd* const qv = lo ? zz : q + 12 + (ph - 6);
-#pragma unroll
-        for (int j = 0; j < 6; ++j) cV[j] = qv[6 * j];
-      };
-      auto cr_apply = [&](double cA, double cT, const double (&cV)[6], double v) __attribute__((always_inline)) {
-        const double vr = dppd<0x128>(v);  // row_ror:8: component ph +- 6 (LN(j + 6) = LN(j) + 8)
-        return bdot_ln6v(cV, v, fma(cT, vr, cA * v));
-      };
-      // P_ab: the reduced right-hand side.  Lanes of even stage k form
-      //   b'_{k/2} = b_k - L_k u_a - L_{k+1}' u_b,  u_a = D_{k-1}^{-1} b_{k-1} (this row),
-      //   u_b = D_{k+1}^{-1} b_{k+1} (the odd row below, its own product, handed up by
-      // permlane16), split over the two halves the sweep sums (RB[q], RB[q + 12 NS]).
-      // Branch-free: every lane computes, the odd rows' stores go to the sink.
-      auto cr_reduce = [&]() __attribute__((always_inline)) {
-        constexpr int NS = CRL<N>::NS;
-        launder();
-        const bool ev = (k & 1) == 0;
-        lds_cd* const BO = (lds_cd*)&sh.u.it.bo[0][0];  // b = bo + na (na at + 12 N)
-        const int kb = ev ? (k >= 1 ? k - 1 : 0) : k;
-        const int sb = 12 * SIG<N>(kb) + ph;
-        const double bv = BO[sb] + BO[sb + 12 * N];
-        const int di = (ev ? (k >= 1 ? k - 1 : 0) : k) >> 1;
-        lds_cd* const Mr = (ev && k == 0) ? (lds_cd*)sh.zero : GHr + (CRL<N>::DI + GS * di + RS * ph);
-        double g[12];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          const dbl2 v = ((lds_cd2*)Mr)[i];
-          g[2 * i] = v.x;
-          g[2 * i + 1] = v.y;
-        }
-        const double so_b = BO[12 * SIG<N>(k) + ph], so_n = BO[12 * SIG<N>(k) + ph + 12 * N];
-        double cA, cT, cV[6], dA, dT, dV[6];
-        cr_lrow(k, cA, cT, cV);
-        cr_lcol(k + 1 <= N - 1 ? k + 1 : N - 1, dA, dT, dV);
-        const double u = bdot_ln12(g, bv, 0.0);  // row ph of D^{-1} b (lane LN(i) holds b[i])
-        double ub;
-        {  // rows 0 <- 1, 2 <- 3: the odd row's u (permlane16_swap's second result)
-          const long long bb = __double_as_longlong(u);
-          const auto lo_ = __builtin_amdgcn_permlane16_swap((unsigned)bb, (unsigned)bb, false, false);
-          const auto hi_ = __builtin_amdgcn_permlane16_swap((unsigned)(bb >> 32), (unsigned)(bb >> 32), false, false);
-          ub = __longlong_as_double(((long long)hi_[1] << 32) | lo_[1]);
-        }
-        const double la = cr_apply(cA, cT, cV, u);
-        const double lb_ = cr_apply(dA, dT, dV, ub);
-        double* const W1 = &sh.u.it.nb[0][0] + (12 * SIG<NS>(k >> 1) + ph);
-        const bool st = cl && ev;
-        *(st ? W1 : Wdump) = (so_b + so_n) - la;
-        *(st ? W1 + 12 * NS : Wdump) = -lb_;
-      };
-      // P_c: the odd stages' states, x_k = D_k^{-1} (b_k - L_k x_{k-1} - L_{k+1}' x_{k+1})
-      // from the reduced sweep's even states; stored after the reduced states (CRL::XO)
-      auto cr_back = [&]() __attribute__((always_inline)) {
-        constexpr int NS = CRL<N>::NS;
-        launder();
-        const bool od = (k & 1) != 0;
-        lds_cd* const XS = (lds_cd*)&sh.u.it.xs[0][0];
-        lds_cd* const BO = (lds_cd*)&sh.u.it.bo[0][0];
-        const bool hn = k + 1 <= N - 1;
-        const double xm = XS[12 * SIGX<NS>(((k >= 1 ? k - 1 : 0) >> 1) + 1) + ph];
-        const double xp = *(hn ? XS + (12 * SIGX<NS>(((k + 1) >> 1) + 1) + ph) : (lds_cd*)sh.zero);
-        double cA, cT, cV[6], dA, dT, dV[6];
-        cr_lrow(k, cA, cT, cV);
-        cr_lcol(hn ? k + 1 : N - 1, dA, dT, dV);
-        lds_cd* const Mr = GHr + (CRL<N>::DI + GS * (k >> 1) + RS * ph);
-        double g[12];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          const dbl2 v = ((lds_cd2*)Mr)[i];
-          g[2 * i] = v.x;
-          g[2 * i + 1] = v.y;
-        }
-        const int so = 12 * SIG<N>(k) + ph;
-        const double bk = BO[so] + BO[so + 12 * N];
-        const double r = (bk - cr_apply(cA, cT, cV, xm)) - cr_apply(dA, dT, dV, xp);
-        const double x = bdot_ln12(g, r, 0.0);
-        double* const Xo = &sh.u.it.xs[0][0] + (CRL<N>::XO + 12 * (k >> 1) + ph);
-        *((cl && od) ? Xo : Wdump) = x;
-      };
-      // the state sweep: the lagging form up to 32 stages (on the reduced system when
-      // kCR), the split form beyond
+      // the state sweep: the lagging form up to 32 stages, the split form beyond
       auto ph_sweep = [&]() __attribute__((always_inline)) {
         if constexpr (BIG) {
           ph_sweep_split();
-        } else if constexpr (CR) {
-          constexpr int NS = CRL<N>::NS;
-          sync_all();  // ph_rhs's right-hand sides
-          STAMP(3);
-          cr_reduce();
-          // (its barrier publishes the reduced right-hand sides)
-          ph_sweep_lag(std::integral_constant<int, NS>{}, std::integral_constant<int, 15>{},
-                       (lds_cd*)&sh.u.it.nb[0][0], 12 * NS, &sh.u.it.yv[0][0], &sh.u.it.xs[0][0]);
-          sync_all();  // the even stages' states
-          STAMP(12);   // (diagnostic builds: the outward sweep and this barrier)
-          cr_back();
-          // (ph_recover's barrier publishes the odd stages' states)
         } else {
           ph_sweep_lag(std::integral_constant<int, N>{}, std::integral_constant<int, 3>{},
                        (lds_cd*)&sh.u.it.bo[0][0], 12 * N, &sh.u.it.yv[0][0], &sh.u.it.xs[0][0]);
@@ -3069,15 +2570,12 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         // their own without them, so the check / infeasibility code and its live values
         // sit outside the hot loop's register allocation (inside it, they cost 0.31 us
         // per iteration through spills on the sweep path, measured).
-        // MODE 0: a plain iteration; 1 (DELTA): the checked one, also keeping delta_y / delta_x;
-        // 2 (CARRY, kDC): the iteration after a deferred check, which evaluates that check
-        // between its sweep and its update and returns before the update (*stop = the
-        // status) when it ends the solve
+        // MODE 0: a plain iteration; 1 (DELTA): the checked one, also keeping delta_y / delta_x
         auto admm_iter = [&](auto mode_tag, const RhsOps& ops, double (&dyv)[3], double& dxf_, double& dxX_,
-                             double (&cvp)[CK_COUNT], int* stop)
+                             double (&cvp)[CK_COUNT])
             __attribute__((always_inline)) {
           constexpr int MODE = decltype(mode_tag)::value;
-          constexpr bool DELTA = MODE == 1, CARRY = MODE == 2;
+          constexpr bool DELTA = MODE == 1;
           double uf, beta, sf, sX, ax[3];
           // (beyond 32 stages the operands are read per iteration: held, they cost the
           // register budget of the 9..16-wave workgroups -- N = 48: scratch 840 -> 712 B
@@ -3087,11 +2585,6 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // DELTA (the last iteration before a check): the check's constant block is read
           // here, its memory latency behind the force recovery and the z / y / x update
           if constexpr (DELTA) ck_all(cvp);
-          // CARRY: the deferred check's residual terms, on waves 1.. while wave 0 sweeps
-          if constexpr (CARRY) {
-            ck_all(cvp);
-            dc_terms(cvp);
-          }
           double zl[3], zh[3], zrr[3], zri[3];  // the update's per-row constants
           if constexpr (kZcMem<N>) {
             ph_recover(nullptr, zc_ptr()[ZC_RI], uf, beta, sf, sX, ax);
@@ -3104,25 +2597,6 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             ph_recover(kBig<N> ? nullptr : &ops, ri[0], uf, beta, sf, sX, ax);
 #pragma unroll
             for (int j = 0; j < 3; ++j) { zl[j] = lo_of(j); zh[j] = hi_of(j); zrr[j] = rr[j]; zri[j] = ri[j]; }
-          }
-          if constexpr (CARRY) {
-            // (ph_recover's barrier published every wave's terms) osqp's check_termination
-            // on the checked iteration, then the infeasibility products where needed
-            info_combine(std::true_type{}, cvp, sh.dcp, 24);
-            int st = 0;
-            if (!(isfinite(pri_res) && isfinite(dua_res))) {
-              st = MPCQ_STATUS_NONFINITE;
-            } else if (converged(1.0)) {
-              st = MPCQ_STATUS_SOLVED;
-            } else {
-              if (inf_need) dc_products(cvp);
-              if (inf_bits & 1) st = MPCQ_STATUS_PRIMAL_INFEASIBLE;
-              else if (inf_bits & 2) st = MPCQ_STATUS_DUAL_INFEASIBLE;
-            }
-            if (st != 0) {
-              *stop = st;
-              return;
-            }
           }
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
@@ -3143,7 +2617,6 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         };
         const bool chk_on = p.check_termination > 0;
         const bool adp_on = p.adaptive_rho && p.adaptive_rho_interval > 0;
-        bool dc_pending = false;  // (kDC) the previous iteration's check awaits its carrier
         while (iter <= p.max_iter) {
           // the next event: a termination check, an adaptive-rho step or the last iteration
           int until = p.max_iter - iter + 1;
@@ -3155,45 +2628,16 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           RhsOps ops;
           if constexpr (!kBig<N>) load_rhs_ops(ops);
           double cvp[CK_COUNT];
-          int r0 = 1;
-          if constexpr (kDC<N>) {
-            if (dc_pending) {  // this segment's first iteration carries the deferred check
-              dc_pending = false;
-              int st = 0;
-              admm_iter(std::integral_constant<int, 2>{}, ops, dyv, dxf_, dxX_, cvp, &st);
-              if (st != 0) {  // the check of the previous iteration ends the solve there
-                MPCQ_SET_XST(st);
-                --iter;
-                break;
-              }
-              r0 = 2;
-              ++iter;
-            }
-          }
 #pragma nounroll
-          for (int r_ = r0; r_ < until; ++r_, ++iter)
-            admm_iter(std::integral_constant<int, 0>{}, ops, dyv, dxf_, dxX_, cvp, nullptr);
-          admm_iter(std::integral_constant<int, 1>{}, ops, dyv, dxf_, dxX_, cvp, nullptr);
+          for (int r_ = 1; r_ < until; ++r_, ++iter)
+            admm_iter(std::integral_constant<int, 0>{}, ops, dyv, dxf_, dxX_, cvp);
+          admm_iter(std::integral_constant<int, 1>{}, ops, dyv, dxf_, dxX_, cvp);
           // iter % check_termination == 0 / iter % adaptive_rho_interval == 0, by countdown
           const bool can_check = chk_on && (to_check -= until) == 0;
           if (can_check) to_check = p.check_termination;
           const bool adapt = adp_on && (to_adapt -= until) == 0;
           if (adapt) to_adapt = p.adaptive_rho_interval;
           last_checked = can_check;
-          if constexpr (kDC<N>) {
-            // a check that is not an adaptive-rho step, followed by an iteration that is not
-            // itself an event, is deferred into that iteration (the carrier)
-            int nxt = p.max_iter - iter;
-            if (chk_on && to_check < nxt) nxt = to_check;
-            if (adp_on && to_adapt < nxt) nxt = to_adapt;
-            if (can_check && !adapt && nxt >= 2) {
-              dc_publish(dyv, dxf_, dxX_, cvp);
-              dc_pending = true;
-              STAMP(11);
-              ++iter;
-              continue;
-            }
-          }
           // the last iteration's information is always formed here, while its deltas are
           // live (osqp's update_info after the loop when the last iteration was unchecked)
           infeas_cheap(dyv, dxf_, dxX_, cvp);

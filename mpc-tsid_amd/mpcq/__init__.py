@@ -18,7 +18,7 @@ from ._lib import (FLAG_ASYNC, FLAG_DEVICE_PTRS, MODE_SETUP, MODE_UPDATE,  # noq
                    STATUS_NONFINITE, STATUS_SOLVED, STATUS_SOLVED_INACCURATE, STATUS_PRIMAL_INFEASIBLE,
                    STATUS_DUAL_INFEASIBLE, STATUS_PRIMAL_INFEASIBLE_INACCURATE,
                    STATUS_DUAL_INFEASIBLE_INACCURATE, STATUS_BAD_BOUNDS, MpcqError,
-                   Params, build, default_params, lib, supported_horizons)
+                   Params, build, build_info, default_params, lib, source_sha, supported_horizons)
 from .engine import Engine, dims, pattern  # noqa: F401
 from .session import Session  # noqa: F401
 

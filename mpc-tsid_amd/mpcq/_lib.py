@@ -65,7 +65,8 @@ EXPORTS = ("mpcq_abi_version", "mpcq_default_params", "mpcq_dims", "mpcq_pattern
            "mpcq_set_stream", "mpcq_last_kernel_ms", "mpcq_formulate_batch",
            "mpcq_qp_solve_batch", "mpcq_solve_batch", "mpcq_default_planner_params",
            "mpcq_plan_batch", "mpcq_session_create", "mpcq_session_destroy", "mpcq_session_tick",
-           "mpcq_session_read", "mpcq_session_write", "mpcq_session_device_ptr", "mpcq_debug_set_stamps")
+           "mpcq_session_read", "mpcq_session_write", "mpcq_session_device_ptr", "mpcq_debug_set_stamps",
+           "mpcq_build_info")
 
 
 class MpcqError(RuntimeError):
@@ -188,6 +189,7 @@ def lib():
     L.mpcq_pattern.argtypes = [C.c_int, ip, ip]
     L.mpcq_supported_horizons.argtypes = [ip, C.c_int]
     L.mpcq_last_error.restype = C.c_char_p
+    L.mpcq_build_info.restype = C.c_char_p
     L.mpcq_create.argtypes = [C.c_int, C.c_int, PP, C.POINTER(vp)]
     L.mpcq_destroy.argtypes = [vp]
     L.mpcq_set_stream.argtypes = [vp, vp]
@@ -245,6 +247,23 @@ def default_planner_params(**overrides) -> PlannerParams:
             raise AttributeError(f"unknown planner parameter {k}")
         setattr(p, k, v)
     return p
+
+
+def build_info() -> dict:
+    """The loaded library's build stamp (mpcq_build_info): {"src_sha256": ..., "arch": ...}."""
+    raw = lib().mpcq_build_info().decode()
+    return dict(kv.split("=", 1) for kv in raw.split() if "=" in kv)
+
+
+def source_sha(csrc: str = CSRC) -> str:
+    """The stamp the Makefile computes for the sources in ``csrc``: the first 16 hex
+    digits of sha256 over csrc/*.hip concatenated in name order."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in sorted(n for n in os.listdir(csrc) if n.endswith(".hip")):
+        with open(os.path.join(csrc, name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def supported_horizons():

@@ -45,6 +45,6 @@ def gather_rows(dist, t, total: int, world: int, rank: int):
 def max_over_ranks(dist, value: float, device, world: int) -> float:
     import torch
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
-    if world > 1:
+    if world > 1 or (dist.is_available() and dist.is_initialized()):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -26,5 +26,5 @@ for n in $HS; do OBJS="$OBJS $OUT/$NAME/e$n.o"; HX="$HX X($n)"; done
 printf '#include "mpcq_internal.h"\n#undef MPCQ_HORIZONS\n#define MPCQ_HORIZONS(X) %s\n#include "mpcq_dispatch.cpp"\n' "$HX" > $OUT/$NAME/dispatch.cpp
 /opt/rocm/bin/hipcc $F -I$R/include -c -o $OUT/$NAME/dispatch.o $OUT/$NAME/dispatch.cpp
 /opt/rocm/bin/hipcc $F -shared -o $OUT/libmpcq_$NAME.so $OBJS $C/build/mpcq_planner.o $C/build/mpcq_session.o \
-  $C/build/mpcq_api.o $OUT/$NAME/dispatch.o
+  $C/build/mpcq_api.o $C/build/mpcq_build.o $OUT/$NAME/dispatch.o
 echo "built $OUT/libmpcq_$NAME.so"

@@ -36,6 +36,23 @@ def counters(path, kernel="engine_kernel"):
     return agg
 
 
+def bench_stamp(logpath):
+    """engine_src_sha of the library the profiled bench.py process loaded (its JSON line's
+    "build" object), or None."""
+    try:
+        lines = open(logpath).read().splitlines()
+    except OSError:
+        return None
+    for ln in reversed(lines):
+        ln = ln.strip()
+        if ln.startswith("{") and '"metric"' in ln:
+            try:
+                return (json.loads(ln).get("build") or {}).get("engine_src_sha")
+            except ValueError:
+                return None
+    return None
+
+
 def mean(v):
     return sum(v) / len(v) if v else None
 
@@ -68,9 +85,21 @@ def main():
     kern_ms = (sum(float(r["AverageNs"]) * int(r["Calls"]) for r in eng) /
                max(1, sum(int(r["Calls"]) for r in eng)) / 1e6) if eng else None
 
+    # every pass must have run the same build; the stamp goes into pmc_traffic.json, and
+    # bench.py drops an entry whose stamp differs from the library it is running
+    stamps = {p: bench_stamp(os.path.join(src, f"{p}.log")) for p in ("trace", "fetch", "write", "sq", "sq2", "f64")
+              if os.path.exists(os.path.join(src, f"{p}.log"))}
+    seen = {v for v in stamps.values() if v}
+    if len(seen) > 1:
+        raise SystemExit(f"passes of {a.tag} ran different builds: {stamps}")
+    sha = seen.pop() if seen else None
+    if sha is None:
+        print(f"warning: no build stamp in the bench lines of {src}; the entry stays unstamped (bench.py ignores it)")
+
     fk, wk = mean(fetch.get("FETCH_SIZE", [])), mean(write.get("WRITE_SIZE", []))
     traffic = None
-    lines = [f"# rocprofv3 summary `{a.tag}` ({a.key})", ""]
+    lines = [f"# rocprofv3 summary `{a.tag}` ({a.key})", "",
+             f"- build: libmpcq.so engine_src_sha `{sha}` (mpcq_build_info of the profiled process, every pass)"]
     for r in eng:
         lines.append(f"- kernel `{r['Name']}`: {r['Calls']} calls, average {float(r['AverageNs']) / 1e6:.3f} ms "
                      f"(min {float(r['MinNs']) / 1e6:.3f}, max {float(r['MaxNs']) / 1e6:.3f}), "
@@ -146,6 +175,7 @@ def main():
         except (OSError, ValueError):
             d = {}
         d[a.key] = {"bytes_per_launch": traffic, "fetch_kib": fk, "write_kib": wk, "tag": a.tag,
+                    "engine_src_sha": sha,
                     "fp64_flops_per_launch": fp64_flops, "kernel_ms": kern_ms,
                     "note": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section), separate --pmc passes; "
                             "fp64 flops = (2 SQ_INSTS_VALU_FMA_F64 + ADD_F64 + MUL_F64) x 64 from their own pass"}

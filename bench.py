@@ -175,7 +175,19 @@ def _dist_setup():
             from mpcq import launch
             os.environ["MASTER_PORT"] = str(launch.free_port())
         torch.cuda.set_device(local)
-        dist.init_process_group(backend, init_method="env://", rank=rank, world_size=world)
+        # RCCL prints its version banner on stdout at initialisation: keep stdout for the one
+        # JSON line (the banner goes to stderr)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(backend, init_method="env://", rank=rank, world_size=world)
+            if backend == "nccl":  # the communicator is created lazily: make it now, under the redirect
+                dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     coll = dev if backend == "nccl" else torch.device("cpu")  # where collective tensors live

@@ -614,6 +614,13 @@ constexpr int kFWS = N <= 32 ? 96 : 72;
 // so the status stays a register there.
 template <int N>
 constexpr bool kXstLds = N <= 16;
+// Beyond 16 stages (round 5) the exit status is not carried at all: after the loop it is
+// re-derived from what the loop leaves -- a failed factorisation sets sh.flag[2], and an
+// early exit stops with iter <= max_iter after the same tests, in the same order, on the
+// residuals and infeasibility bits that stay live after the loop anyway.  Carried in a
+// register, it was spilled and stored once per check segment at N = 32 (round 4).
+template <int N>
+constexpr bool kXstRe = !kXstLds<N>;
 template <int N>
 struct Work {  // offsets (doubles) inside one instance's workspace
   // SM starts two slots in (a pad kept from round 2; the sweep no longer reads it)
@@ -2543,7 +2550,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       bool last_checked = false;
       int iter = 1;
       // the loop's exit status: LDS (kXstLds; read after the loop's closing barrier) or status
-#define MPCQ_SET_XST(v_) do { if constexpr (kXstLds<N>) { if (t == 0) sh.flag[4] = (v_); } else { status = (v_); } } while (0)
+#define MPCQ_SET_XST(v_) do { if constexpr (kXstLds<N>) { if (t == 0) sh.flag[4] = (v_); } else if constexpr (!kXstRe<N>) { status = (v_); } } while (0)
       if constexpr (kXstLds<N>) MPCQ_SET_XST(0);
       int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
       // the bounds are re-derived where used (lo_of / hi_of: a select on the lane's
@@ -2671,6 +2678,15 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       if constexpr (kXstLds<N>) {
         sync_all();  // thread 0's exit status
         status = sh.flag[4];
+      }
+      if constexpr (kXstRe<N>) {  // the exit's reason, as the loop tested it (kXstRe)
+        if (sh.flag[2] != 0) status = MPCQ_STATUS_FACTOR_FAILED;
+        else if (iter <= p.max_iter) {
+          if (!(isfinite(pri_res) && isfinite(dua_res))) status = MPCQ_STATUS_NONFINITE;
+          else if (converged(1.0)) status = MPCQ_STATUS_SOLVED;
+          else if (inf_bits & 1) status = MPCQ_STATUS_PRIMAL_INFEASIBLE;
+          else if (inf_bits & 2) status = MPCQ_STATUS_DUAL_INFEASIBLE;
+        }
       }
 #undef MPCQ_SET_XST
       it_done = iter > p.max_iter ? p.max_iter : iter;

@@ -309,6 +309,23 @@ __device__ __forceinline__ double sel3(int i, double a0, double a1, double a2) {
   return i == 0 ? a0 : (i == 1 ? a1 : a2);
 }
 
+// f(integral_constant<int, J>) for J in the sequence, in order
+template <typename F, int... J>
+__device__ __forceinline__ void for_each_j(F&& f, std::integer_sequence<int, J...>) {
+  (f(std::integral_constant<int, J>{}), ...);
+}
+// a0 += v(lane J) g0, a1 += v(lane J) g1, a2 += v(lane J) g2, v broadcast from lane J of the
+// row (v_fmac_f64_dpp; s_nop 1 covers a VALU write of v just before)
+template <int J>
+__device__ __forceinline__ void fmac3_bc(double& a0, double& a1, double& a2, double v, double g0, double g1, double g2) {
+  asm("s_nop 1\n\t"
+      "v_fmac_f64_dpp %0, %3, %4 row_newbcast:%7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %3, %5 row_newbcast:%7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %2, %3, %6 row_newbcast:%7 row_mask:0xf bank_mask:0xf"
+      : "+v"(a0), "+v"(a1), "+v"(a2)
+      : "v"(v), "v"(g0), "v"(g1), "v"(g2), "n"(J));
+}
+
 // Gauss-Jordan inverse of a 12x12 SPD matrix held one row per column lane
 // (row psi in lane LN(psi)); pivots broadcast by row_newbcast, no pivoting.
 // gj_fmac<PV>: the pivot's eleven row updates c[j] += a * R[j](lane LN(PV)), j != PV, as
@@ -604,8 +621,8 @@ template <int N> constexpr bool kLagOut = N <= 48;
 // x 3, stages 0 mod 16 units apart) the twelve rows of each group land in distinct banks.
 // Up to 32 stages, where the LDS has the 24 N doubles (N = 16: 80,048 B, still two
 // instances per CU).
-template <int N>
-constexpr int kFWS = N <= 32 ? 96 : 72;
+template <int N, bool KI = false>
+constexpr int kFWS = (N <= 32 && !KI) ? 96 : 72;  // (kKI: the LDS goes to Z's columns)
 // Up to 16 stages the ADMM loop's exit status goes through LDS (Smem::flag[4]) instead of
 // a register carried across the loop: the N = 16 kernel then spills 27 instead of 43
 // VGPRs (scratch 256 -> 224 B per lane) and its C2 HBM traffic falls 127 -> 88 MB per
@@ -621,6 +638,61 @@ constexpr bool kXstLds = N <= 16;
 // register, it was spilled and stored once per check segment at N = 32 (round 4).
 template <int N>
 constexpr bool kXstRe = !kXstLds<N>;
+// ---- The explicit state-system inverse (kKI, round 5) ------------------------------
+// At 16 stages the ADMM loop solves the state system K_s x = r (192 x 192, block
+// tridiagonal) with an explicit inverse Z = K_s^{-1} instead of the two-ended sweep: one
+// dense matrix-vector product spread over every wave (no serial chain of N/2 dependent
+// 12 x 12 steps on one wave).  Z is formed once per factorisation from the sweep's own
+// factors (G / H / S^{-1} / M^{-1}): the sweep run on the identity's columns, 16 columns
+// at a time as 16 x 16 x 12 products on v_mfma_f64_16x16x4_f64, both chains of a tile in
+// one wave.  The workgroup doubles to eight waves (one instance per CU, 256 VGPRs): waves
+// 0-3 hold the stages as before, waves 4-7 ("helpers") hold 138 of Z's 192 columns in
+// registers (105 doubles per lane); the other 54 columns sit in LDS (KV) and waves 0-3
+// multiply them.  The helpers run the stage waves' barrier sequence with no stage work
+// (factor / checks with role std::true_type) and take part only in the formation and the
+// product.  The oracle's explicit-inverse restatement (full K^{-1} on the C2 and a mixed
+// 4096-instance batch) kept statuses and iteration counts identical to its factored solve,
+// forces within 1.5e-9.
+// Measured and NOT the default (round 5, profiles/r05b_*, r05e_*): parity green on the GPU
+// suite (79/79, statuses and iterations = the oracle's), but 1.92 us per iteration alone
+// against the sweep's 1.85, and one instance per CU instead of two: C2 86 k, C4 104 k, C5 135 k
+// QP/s against 126 k / 222 k / 285 k.  The product is 36,864 FMAs per iteration (ten times
+// the sweep's) and its FP64 issue, not a serial chain, then bounds the iteration; the stage
+// waves' own instruction stream (right-hand sides, forces, update: ~250 instructions) stays
+// on the critical path either way.  Build with -DMPCQ_KINV (make variants compiles it).
+#ifdef MPCQ_KINV
+template <int N>
+constexpr bool kKinv = N == 16;
+#else
+template <int N>
+constexpr bool kKinv = false;
+#endif
+template <int N, bool SOLVE, bool POLISH>
+constexpr bool kKI = kKinv<N> && SOLVE && !POLISH;
+template <int N>
+struct KinvLay {
+  static constexpr int R = 12 * N;             // states (rows / columns of Z)
+  static constexpr int KVS = R + 1;            // column stride of KV (odd: conflict-free columns)
+  static constexpr int HC = 34;                // helper register columns (per lane: rows l, l+64, l+128)
+  static constexpr int SC = 14;                // stage wave LDS columns
+  static constexpr int SP0 = 4 * HC, SPC = R - SP0;  // the LDS part: columns 136..191
+  // helper h's columns [hc0, hc0 + hcn), stage wave s's [sc0, sc0 + scn)
+  __host__ __device__ static constexpr int hc0(int h) { return HC * h; }
+  __host__ __device__ static constexpr int hcn(int) { return HC; }
+  __host__ __device__ static constexpr int sc0(int s_) { return SP0 + SC * s_; }
+  __host__ __device__ static constexpr int scn(int) { return SC; }
+  // formation passes: columns [pc0, pc0 + pcn) staged in KV (the last pass is KV's own part)
+  static constexpr int NPASS = 4;
+  __host__ __device__ static constexpr int pc0(int q) { return q < 3 ? 48 * q : SP0; }
+  __host__ __device__ static constexpr int pcn(int q) { return q < 2 ? 48 : (q == 2 ? SP0 - 96 : SPC); }
+};
+static_assert(KinvLay<16>::hc0(3) + KinvLay<16>::hcn(3) == KinvLay<16>::SP0 &&
+                  KinvLay<16>::sc0(3) + KinvLay<16>::scn(3) == KinvLay<16>::R && KinvLay<16>::pcn(3) <= 64 &&
+                  KinvLay<16>::pc0(2) + KinvLay<16>::pcn(2) == KinvLay<16>::SP0 && KinvLay<16>::pcn(3) <= 56 &&
+                  KinvLay<16>::hc0(3) + 47 < KinvLay<16>::R,
+              "Z's column split");
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
 template <int N>
 struct Work {  // offsets (doubles) inside one instance's workspace
   // SM starts two slots in (a pad kept from round 2; the sweep no longer reads it)
@@ -629,7 +701,7 @@ struct Work {  // offsets (doubles) inside one instance's workspace
                        FR = AB + (kAbG<N> ? ((126 * N - 18 + 1) & ~1) : 0), SIZE = FR + (N > 48 ? 12 * 16 * kRows<N> : 0);
 };
 
-template <int N>
+template <int N, bool KI = false>
 struct Smem {
   double Ab[kAbG<N> ? 2 : 126 * N - 18];  // scaled constraint values, CSC order (N > 49: Work<N>::AB)
   // GH[0] = M^{-1}, GH[SIG(k)] = G_k (1 <= k <= m), GH[SIG(k+1)] = H_k (m <= k < N-1),
@@ -644,7 +716,7 @@ struct Smem {
   double Smpad[2];
   // F_k W_k (12x6, row psi at [6 psi]); W_k = B_k' R on rows 6..11: here beyond 32 stages
   // (stage stride 72), FWs at the end up to 32 stages (stride kFWS = 96)
-  alignas(16) double FWb[kBig<N> ? N : 1][72];
+  alignas(16) double FWb[kBig<N> ? N : 1][(kBig<N> || !KI) ? 72 : 2];  // (kKI: no room for the placeholder)
   double QL[kBig<N> ? 1 : N][36];   // B_k F_k W_k = R^{-1} W_k' F_k W_k (6x6)
   union {
     struct {
@@ -668,14 +740,17 @@ struct Smem {
   double dump[64];          // sink of predicated stores (never read): lane & 63
   // (13 unused doubles: where round 4's deferred-check arrays sat; they keep every later
   // array's LDS offset, and with it the compiler's register allocation, as measured)
-  double pad13_[13];
+  double pad13_[KI ? 1 : 13];
   alignas(16) double zero[72];  // zeros: masked coefficient reads point here instead of selecting
   // flag[4] (kXstLds): the ADMM loop's exit status, written by thread 0 at the (uniform)
   // exits and read by every thread after the loop
   int flag[kXstLds<N> ? 5 : 4];
   // (up to 32 stages) F W at its 96-double stride, last: its round-4 growth leaves every
   // other array's LDS offset -- and the compiler's register allocation -- as before
-  alignas(16) double FWs[kBig<N> ? 1 : N][kBig<N> ? 2 : kFWS<N>];
+  alignas(16) double FWs[kBig<N> ? 1 : N][kBig<N> ? 2 : kFWS<N, KI>];
+  // (kKI) Z's LDS part, column-major (column c - SP0 at KVS (c - SP0)); during the
+  // formation the staging of each pass.  The loop's partial products P[wave][row] sit in GH.
+  alignas(16) double KV[KI ? KinvLay<N>::SPC * KinvLay<N>::KVS : 1];
 };
 
 // prologue aliases inside GH
@@ -691,16 +766,20 @@ struct Prologue {
 // !FUSED: solve the given (Ax, l, u).  SOLVE=false: formulation only.
 
 template <int N, bool FUSED, bool SOLVE, bool POLISH>
-__global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p, LaunchArgs a) {
-  constexpr int NR = kRows<N>, NW = NR / 4, T = 16 * NR, n = 24 * N, m = 44 * N, nnz = 126 * N - 18, MID = N / 2;
+__global__ __launch_bounds__((16 * kRows<N> * (kKI<N, SOLVE, POLISH> ? 2 : 1)), (kKI<N, SOLVE, POLISH> ? 1 : 2))
+void engine_kernel(mpcq_params p, LaunchArgs a) {
+  // KI: the explicit inverse (kKI): twice the threads, waves NW.. are the helpers
+  constexpr bool KI = kKI<N, SOLVE, POLISH>;
+  constexpr int NR = kRows<N>, NW = NR / 4, T = 16 * NR * (KI ? 2 : 1), n = 24 * N, m = 44 * N, nnz = 126 * N - 18,
+                MID = N / 2;
 #ifndef MPCQ_STAMP_WAVE
 #define MPCQ_STAMP_WAVE 0
 #endif
-  [[maybe_unused]] constexpr int kStampT = 64 * (MPCQ_STAMP_WAVE < NW ? MPCQ_STAMP_WAVE : NW - 1);
+  [[maybe_unused]] constexpr int kStampT = 64 * (MPCQ_STAMP_WAVE < T / 64 ? MPCQ_STAMP_WAVE : T / 64 - 1);
   // the two chains of the state sweeps: top stages 0..MID-1, bottom N-1..MID+1
   // (BOT stages: MID - 1 for even N, MID for odd N), meeting at stage MID
   constexpr int BOT = N - 1 - MID;
-  __shared__ Smem<N> sh;
+  __shared__ Smem<N, KI> sh;
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
   // lane coordinates; the loops launder them (see launder()) so that the
   // compiler recomputes the many LDS offsets derived from them instead of
@@ -1126,17 +1205,22 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
 
     // pr: per-own-row rho override (polish: 1/delta on active rows, 0 elsewhere);
     // nullptr in the ADMM loop, where the class rho applies
-    auto factor = [&](double sigma, const double* pr) __attribute__((always_inline)) -> bool {
+    // role: std::false_type for the stage waves; std::true_type (kKI's helper waves) runs the
+    // same barrier sequence with no work, so both roles pass every barrier together
+    auto factor = [&](auto role, double sigma, const double* pr) __attribute__((always_inline)) -> bool {
+      constexpr bool H = decltype(role)::value;
       bool ok = true;
       launder();
       auto rho_of = [&](int j) __attribute__((always_inline)) -> double {
         return pr ? pr[j] : rho_of_cls(j);
       };
       double* gk = gh0 + GS * k;
-      if (cl) gk[108 + ph] = rho_of(0);
+      if constexpr (!H) {
+        if (cl) gk[108 + ph] = rho_of(0);
+      }
       sync_all();
       // ---- phase P: F_k = K_ff^{-1} (row ph per column lane), F_k W_k, Q_k
-      {
+      if constexpr (!H) {
         double rd6[6];
 #pragma unroll
         for (int j = 0; j < 6; ++j) rd6[j] = gk[114 + j];
@@ -1188,7 +1272,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         }
         if (cl) {
 #pragma unroll
-          for (int j = 0; j < 6; ++j) { gk[36 + 6 * ph + j] = fw[j]; FWW[kFWS<N> * k + 6 * ph + j] = fw[j]; }
+          for (int j = 0; j < 6; ++j) { gk[36 + 6 * ph + j] = fw[j]; FWW[kFWS<N, KI> * k + 6 * ph + j] = fw[j]; }
         }
         wave_sync();
         // Q = W' (F W): 36 entries over the row's 16 lanes
@@ -1283,7 +1367,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         launder();
         const bool mid = j == MID;
         const bool top = !mid && k == j, bot = !mid && k == N - 1 - j && k > MID, mrow = mid && k == MID;
-        if (top || bot || mrow) {
+        if (!H && (top || bot || mrow)) {
           const bool useT = (top && k > 0) || mrow, useB = (bot && k < N - 1) || mrow;
           double Ro[12];
 #pragma unroll
@@ -1354,8 +1438,8 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       o.oFa = FO<N>(k, f, ta >> 1) + 5 + (ta & 1);
       o.oFb = FO<N>(k, f, 2) + 5 + ta;
       o.oF4 = FO<N>(k, f, 2) + 9;
-      o.oFW = kFWS<N> * k + 6 * ph;
-      const int oFWc = kFWS<N> * k + (isv_ ? ph - 6 : 0);
+      o.oFW = kFWS<N, KI> * k + 6 * ph;
+      const int oFWc = kFWS<N, KI> * k + (isv_ ? ph - 6 : 0);
       o.oQL = 36 * k + 6 * (isv_ ? ph - 6 : 0);
       o.oXSp = 12 * k + ph;  // natural order (update_info)
       o.oXSp6 = 12 * k + (ph < 6 ? ph + 6 : ph);
@@ -1369,8 +1453,13 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       o.oFWcm = isv_ ? oFWc : zFW;
       o.oQLm = isv_ ? o.oQL : zQL;
       o.oB0 = FO<N>(k, 0, 0) + (ph >= 9 ? ph - 8 : 0);  // B row ph on force (fp, cp): + 24 fp + 7 cp
-      o.Wbo = &sh.u.it.bo[SIG<N>(k)][ph];
-      o.Wna = &sh.u.it.na[SIG<N>(hp_ ? k - 1 : N - 1)][ph];
+      if constexpr (KI) {  // natural stage order: the product reads them by state index
+        o.Wbo = &sh.u.it.bo[k][ph];
+        o.Wna = &sh.u.it.na[hp_ ? k - 1 : N - 1][ph];
+      } else {
+        o.Wbo = &sh.u.it.bo[SIG<N>(k)][ph];
+        o.Wna = &sh.u.it.na[SIG<N>(hp_ ? k - 1 : N - 1)][ph];
+      }
       return o;
     };
     const LaneOffs O0 = offs();
@@ -1385,7 +1474,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
   [[maybe_unused]] double* const Wbo = O_.Wbo;                                                             \
   [[maybe_unused]] double* const Wna = O_.Wna
     // beyond 32 stages the loop phases re-derive them too
-    constexpr bool kRecompLoop = BIG;
+    constexpr bool kRecompLoop = BIG || KI;  // (kKI: the helpers' registers set the budget)
     auto launder_p = [&]() __attribute__((always_inline)) {
       lds_uniform(Ab); lds_uniform(GHr); lds_uniform(SmR); lds_uniform(FWr); lds_uniform(QLr); lds_uniform(XSr);
     };
@@ -1657,9 +1746,13 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
     };
     // the products, where a cheap condition holds (inf_need != 0, uniform): A' dy for
     // the primal test, A dx for the dual one, on the deltas infeas_cheap published
-    auto infeas_products = [&](double dxf, double dxX, const double (&cv)[CK_COUNT]) __attribute__((always_inline)) {
+    // role: std::true_type (kKI's helpers) passes the barriers and forms the uniform bits only
+    auto infeas_products = [&](auto role, double dxf, double dxX, const double (&cv)[CK_COUNT])
+        __attribute__((always_inline)) {
+      constexpr bool H = decltype(role)::value;
       MPCQ_CHECK_IDS();
       launder_p();
+      if constexpr (!H) {
       double vu = -INFINITY, vl = -INFINITY;
       {
         double adx[3], lob[3], hib[3];
@@ -1682,6 +1775,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       // lanes 0 / 4 / 8 keep ||D^-1 A' dy|| / vu / vl, published in slots 1 / 4 / 5
       const double mine = pair_max(row_pair_max(tred3(naty, vu, vl, s)));
       if (lane == 0 || lane == 4 || lane == 8) sh.red[32 * wv + 16 + (lane == 0 ? 1 : 4 + (lane >> 3))] = mine;
+      }
       sync_all();
       const int e = s < 6 ? s : 0;  // slots 16..21 are all maxima (0 / 2 / 3 from infeas_cheap)
       double v = sh.red[16 + e];
@@ -2000,8 +2094,11 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       };
       // o: the operands held in registers (the ADMM loop), or null: read them here (polish,
       // whose loop would otherwise spill them)
+      // rsum (kKI): r = bo + na summed in LDS (two ds_add_f64 into a zeroed slot: its two
+      // addends commute, so the sum's bits do not depend on which lane adds first) instead of
+      // bo / na stored apart -- the product then loads one value per column, not two and an add
       auto ph_rhs = [&](bool admm, const RhsOps* op, const double (&pw)[3], double xcf, double xcX, double& uf,
-                        double& beta) __attribute__((always_inline)) {
+                        double& beta, lds_d* rsum = nullptr) __attribute__((always_inline)) {
           launder_p();
           RhsOps own_;
           if (!op) load_rhs_ops(own_);
@@ -2053,12 +2150,20 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
             const double nb = cH6 * w[0];                // H6(k, ph): on X_k[ph+6] (ph < 6)
             // stage 0 zeroes the last stage's na / nb (that stage has no next stage:
             // its coefficients read zero)
-            *(cl ? Wbo : Wdump) = bo;
+            if (!(KI && rsum)) *(cl ? Wbo : Wdump) = bo;
             // stage k-1's component r takes na of lane r and nb of the lane 8 away in the
             // row (component r -+ 6, LN): summed here, one value and one add less per
             // sweep step
             const double nbx = dppd<0x128>(nb);  // row_ror:8
-            *(cl ? Wna : Wdump) = na + nbx;
+            if (KI && rsum) {
+              if (cl) {
+                __hip_atomic_fetch_add(rsum + 12 * k + ph, bo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(rsum + 12 * (k >= 1 ? k - 1 : N - 1) + ph, na + nbx, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+              }
+            } else {
+              *(cl ? Wna : Wdump) = na + nbx;
+            }
           }
           // (the barrier that publishes bo / na / nb opens ph_sweep)
       };
@@ -2492,6 +2597,15 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
                        (lds_cd*)&sh.u.it.bo[0][0], 12 * N, &sh.u.it.yv[0][0], &sh.u.it.xs[0][0]);
         }
       };
+      // (kKI) the state x_i = sum over the eight waves' partial products P[w][i] (in GH), always
+      // in wave order, so every lane that reads a state gets the same bits
+      auto ki_psum = [&](int i) __attribute__((always_inline)) -> double {
+        lds_cd* const q = GHr + i;
+        double v = q[0];
+#pragma unroll
+        for (int w = 1; w < 2 * NW; ++w) v += q[12 * N * w];
+        return v;
+      };
       // ri0: 1/rho of the own slot-0 row (the ADMM loop's, or polish's)
       auto ph_recover = [&](const RhsOps* op, double ri0, double uf, double beta, double& sf, double& sX,
                             double (&ax)[3])
@@ -2516,8 +2630,18 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           const double cFb = Ab[oFb], cFa = Ab[oFa], cF4 = Ab[oF4], cSw = op ? op->cf[4] : Ab[oF + 4];
           sync_all();
           STAMP(7);
-          const double xa = XSr[rXSpm], xb = XSr[rXSp6m];  // (stage 0: X_0 = 0, a zero slot)
-          sX = XSr[rXS];
+          double xa, xb;
+          if constexpr (KI) {  // the explicit inverse's product (stage 0: X_0 = 0)
+            const int ip = 12 * (hp ? k - 1 : k);
+            sX = ki_psum(12 * k + ph);
+            const double a_ = ki_psum(ip + ph), b_ = ki_psum(ip + (ph < 6 ? ph + 6 : ph));
+            xa = hp ? a_ : 0.0;
+            xb = hp ? b_ : 0.0;
+          } else {
+            xa = XSr[rXSpm];  // (stage 0: X_0 = 0, a zero slot)
+            xb = XSr[rXSp6m];
+            sX = XSr[rXS];
+          }
           asm volatile("" : : : "memory");
           {
             gv = eXd * sX + eHd * xa;  // used from the lanes of rows 6..11 only
@@ -2544,6 +2668,188 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
       };
       const double kNoW[3] = {0.0, 0.0, 0.0};
 
+      // ---- (kKI) the explicit inverse Z = K_s^{-1}: formation and product ----------------
+      using KL = KinvLay<N>;
+      // the wave index as a wave-uniform (scalar) value: the roles and column ranges branch on it
+      auto wvu = [&]() __attribute__((always_inline)) -> int { return __builtin_amdgcn_readfirstlane(t >> 6); };
+      // the summed right-hand side of iteration parity b (kKI): u.it.nb (b = 0) / u.it.yv (b = 1),
+      // free during the iterations (the checks publish there, then zero them again)
+      auto ki_rsum = [&](int b_) __attribute__((always_inline)) -> lds_d* {
+        return (lds_d*)(b_ ? &sh.u.it.yv[0][0] : &sh.u.it.nb[0][0]);
+      };
+      // One 16-column tile of Z (columns cb .. cb + 15) by the two-ended sweep on the
+      // identity's columns, both chains in this wave, every block product a 16 x 16 x 12
+      // MFMA (v_mfma_f64_16x16x4_f64 x 3).  Tiles in the D layout: lane l holds rows
+      // (l >> 4) + 4 r, r = 0..3, of column l & 15 (rows 12..15 are zero); a result's register
+      // s is the next product's B operand for K-slice s, so a chain step moves no data.
+      // A operands: lane l supplies M[l & 15][4 s + (l >> 4)] (transposed: M[4 s + (l >> 4)][l & 15]).
+      // The step's w = S^{-1} y tiles are parked in KV at the columns' own rows and read back
+      // by the outward steps, which overwrite them with the results (the pass's staging):
+      //   top    y_0 = e_0, y_k = e_k - G_k y_{k-1} (k <= MID), w_k = S_k^{-1} y_k (k < MID)
+      //   bottom v_{N-1} = e_{N-1}, v_k = e_k - H_k v_{k+1} (k >= MID), w_k = U_k^{-1} v_k (k > MID)
+      //   x_MID = M^{-1} (y_MID + v_MID - e_MID)
+      //   x_k = w_k - G_{k+1}' x_{k+1} (k < MID),  x_k = w_k - H_{k-1}' x_{k-1} (k > MID)
+      // (-G, -H are stored negated: every step is an accumulation.)
+      auto ki_tile = [&](int c0, int cn, int cb) __attribute__((always_inline)) {
+        const int l = lane, cc = l & 15, rb = l >> 4;
+        const int c = cb + cc;                    // this lane's column of Z
+        const bool keep = c < c0 + cn;            // columns past the pass are computed, not stored
+        double* const col = &sh.KV[0] + KL::KVS * (keep ? c - c0 : 0) + rb;  // + 12 k + 4 r: row 12 k + rb + 4 r
+        const dbl4 zero4 = {0.0, 0.0, 0.0, 0.0};
+        auto e_of = [&](int kk) __attribute__((always_inline)) -> dbl4 {  // the identity's rows of stage kk
+          dbl4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (r < 3 && 12 * kk + rb + 4 * r == c) ? 1.0 : 0.0;
+          return v;
+        };
+        // acc + M x (M 12 x 12 row-major in LDS at q; tr: M') for a tile x in the D layout
+        auto mm = [&](const double* q, bool tr, const dbl4& x, dbl4 acc) __attribute__((always_inline)) -> dbl4 {
+#pragma unroll
+          for (int s_ = 0; s_ < 3; ++s_) {
+            const int o = tr ? 12 * (4 * s_ + rb) + cc : 12 * cc + 4 * s_ + rb;
+            const double av = cc < 12 ? q[cc < 12 ? o : 0] : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, x[s_], acc, 0, 0, 0);
+          }
+          return acc;
+        };
+        auto park = [&](int kk, const dbl4& v) __attribute__((always_inline)) {
+          if (keep) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) col[12 * kk + 4 * r] = v[r];
+          }
+        };
+        auto unpark = [&](int kk) __attribute__((always_inline)) -> dbl4 {
+          dbl4 v = zero4;
+          if (keep) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) v[r] = col[12 * kk + 4 * r];
+          }
+          return v;
+        };
+        const double* const smp = &sh.Sm[0][0];
+        dbl4 yT = e_of(0), vB = e_of(N - 1);
+        park(0, mm(smp + SLOT<N>(SIG<N>(0)), false, yT, zero4));
+        park(N - 1, mm(smp + SLOT<N>(SIG<N>(N - 1)), false, vB, zero4));
+#pragma unroll
+        for (int kk = 1; kk <= MID; ++kk) {
+          yT = mm(gh0 + SLOT<N>(SIG<N>(kk)), false, yT, e_of(kk));
+          if (kk < MID) park(kk, mm(smp + SLOT<N>(SIG<N>(kk)), false, yT, zero4));
+          const int kb = N - 1 - kk;
+          if (kb >= MID) {
+            vB = mm(gh0 + SLOT<N>(SIG<N>(kb + 1)), false, vB, e_of(kb));
+            if (kb > MID) park(kb, mm(smp + SLOT<N>(SIG<N>(kb)), false, vB, zero4));
+          }
+        }
+        const dbl4 em = e_of(MID);
+        dbl4 t4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t4[r] = (yT[r] + vB[r]) - em[r];
+        const dbl4 xm = mm(gh0, false, t4, zero4);  // M^{-1} in GH slot 0
+        park(MID, xm);
+        dbl4 xT = xm, xB = xm;
+#pragma unroll
+        for (int j = 1; j <= (MID > N - 1 - MID ? MID : N - 1 - MID); ++j) {
+          const int kt = MID - j, kb = MID + j;
+          if (kt >= 0) {
+            xT = mm(gh0 + SLOT<N>(SIG<N>(kt + 1)), true, xT, unpark(kt));
+            park(kt, xT);
+          }
+          if (kb <= N - 1) {
+            xB = mm(gh0 + SLOT<N>(SIG<N>(kb)), true, xB, unpark(kb));
+            park(kb, xB);
+          }
+        }
+      };
+      // Z after a factorisation: four passes of at most 54 columns staged in KV (the last
+      // pass is KV's own part); a helper copies the columns it owns from each staged pass.
+      // Both roles run the same barriers.
+      auto kinv_form = [&](auto role, double (&kv)[3 * KL::HC]) __attribute__((always_inline)) {
+        constexpr bool H = decltype(role)::value;
+        if constexpr (!H) {  // the summed right-hand sides start from zero (their barriers follow)
+          if (cl) { ki_rsum(0)[12 * k + ph] = 0.0; ki_rsum(1)[12 * k + ph] = 0.0; }
+        }
+#pragma nounroll
+        for (int q = 0; q < KL::NPASS; ++q) {
+          const int c0 = KL::pc0(q), cn = KL::pcn(q);
+          if constexpr (!H) {
+            const int w_ = wvu();
+            if (w_ * 16 < cn) ki_tile(c0, cn, c0 + 16 * w_);
+          }
+          sync_all();
+          if constexpr (H) {
+            if (q < KL::NPASS - 1) {
+              const int h = wvu() - NW, hc = KL::hc0(h), hn = KL::hcn(h);
+#pragma unroll
+              for (int j = 0; j < KL::HC; ++j) {
+                const int cj = hc + j;
+                if (j < hn && cj >= c0 && cj < c0 + cn) {
+                  const double* const src = &sh.KV[0] + KL::KVS * (cj - c0) + lane;
+                  kv[3 * j] = src[0];
+                  kv[3 * j + 1] = src[64];
+                  kv[3 * j + 2] = src[128];
+                }
+              }
+            }
+          }
+          sync_all();
+        }
+      };
+      // x = Z r, r = bo + na (the state right-hand sides ph_rhs published): this wave's
+      // columns times r into P[wave][row] (rows lane, lane + 64, lane + 128), in column order.
+      // Helpers: their register columns; stage waves: their KV columns.
+      // x = Z r: r is loaded once, distributed (lane s of every 16-lane row holds r of the
+      // wave's column 16 u + s), and each column's three FMAs take it by row broadcast
+      // (v_fmac_f64_dpp row_newbcast:s): no per-column LDS load.  Helpers multiply their
+      // register columns; stage waves load their KV columns in two halves (all issued before
+      // the first half's FMAs).  Three accumulation chains (rows lane, lane + 64, lane + 128),
+      // each in column order.
+      auto kinv_mv = [&](auto role, const double (&kv)[3 * KL::HC], lds_cd* const rs) __attribute__((always_inline)) {
+        constexpr bool H = decltype(role)::value;
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+        // (lane ids from a laundered thread index: held across the loop they were spilled)
+        int tl_ = t;
+        asm volatile("" : "+v"(tl_));
+        const int ln_ = tl_ & 63, s16 = tl_ & 15;
+        if constexpr (H) {
+          const int h = wvu() - NW, hn = KL::hcn(h);
+          lds_cd* const rq = rs + KL::hc0(h);  // (hc0 + 47 < 192: in the buffer)
+          double rv[3];
+#pragma unroll
+          for (int u = 0; u < 3; ++u) rv[u] = rq[16 * u + s16];
+          auto col = [&](auto jt) __attribute__((always_inline)) {
+            constexpr int j = decltype(jt)::value;
+            if (j < KL::HC - 1 || j < hn)
+              fmac3_bc<j % 16>(a0, a1, a2, rv[j / 16], kv[3 * j], kv[3 * j + 1], kv[3 * j + 2]);
+          };
+          for_each_j(col, std::make_integer_sequence<int, KL::HC>{});
+        } else {
+          const int w_ = wvu(), sc = KL::sc0(w_), sn = KL::scn(w_);
+          lds_cd* const kq = (lds_cd*)&sh.KV[0] + KL::KVS * (sc - KL::SP0) + ln_;
+          const double rv = rs[sc + (s16 < sn ? s16 : 0)];
+          constexpr int HALF = 7;
+          double ka[3 * HALF], kb[3 * HALF];
+#pragma unroll
+          for (int i = 0; i < HALF; ++i) {
+            const int ja = i, jb = HALF + i < sn ? HALF + i : sn - 1;  // (clamped: no read past KV)
+            ka[3 * i] = kq[KL::KVS * ja]; ka[3 * i + 1] = kq[KL::KVS * ja + 64]; ka[3 * i + 2] = kq[KL::KVS * ja + 128];
+            kb[3 * i] = kq[KL::KVS * jb]; kb[3 * i + 1] = kq[KL::KVS * jb + 64]; kb[3 * i + 2] = kq[KL::KVS * jb + 128];
+          }
+          asm volatile("" ::: "memory");
+          auto col = [&](auto jt, const double (&kk)[3 * HALF]) __attribute__((always_inline)) {
+            constexpr int j = decltype(jt)::value, i = j % HALF;
+            if (j < 2 * HALF - 1 || j < sn) fmac3_bc<j>(a0, a1, a2, rv, kk[3 * i], kk[3 * i + 1], kk[3 * i + 2]);
+          };
+          for_each_j([&](auto jt) __attribute__((always_inline)) { col(jt, ka); }, std::make_integer_sequence<int, HALF>{});
+          for_each_j([&](auto jt) __attribute__((always_inline)) {
+            col(std::integral_constant<int, HALF + decltype(jt)::value>{}, kb);
+          }, std::make_integer_sequence<int, HALF>{});
+        }
+        double* const P = gh0 + 12 * N * wvu() + ln_;
+        P[0] = a0;
+        P[64] = a1;
+        P[128] = a2;
+      };
+
       // ------------------------------------------------------------ ADMM
       // The factorisation sits outside the hot loop: the outer loop factors,
       // the inner loop iterates until convergence, max_iter or a rho update.
@@ -2553,6 +2859,136 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
 #define MPCQ_SET_XST(v_) do { if constexpr (kXstLds<N>) { if (t == 0) sh.flag[4] = (v_); } else if constexpr (!kXstRe<N>) { status = (v_); } } while (0)
       if constexpr (kXstLds<N>) MPCQ_SET_XST(0);
       int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
+      if constexpr (KI) {
+        // (kKI) the loop of the explicit inverse: one driver for both roles, the helpers
+        // (waves NW..) with std::true_type -- the same barriers and the same uniform
+        // decisions (info_combine reads the stage waves' partials from LDS), no stage work
+        auto kinv_admm = [&](auto role) __attribute__((always_inline)) {
+          constexpr bool H = decltype(role)::value;
+          double kv[3 * KL::HC];  // (helpers) Z's columns hc0.. : rows lane, lane + 64, lane + 128
+#pragma unroll
+          for (int j = 0; j < 3 * KL::HC; ++j) kv[j] = 0.0;
+          const bool chk_on = p.check_termination > 0;
+          const bool adp_on = p.adaptive_rho && p.adaptive_rho_interval > 0;
+          for (;;) {
+            if (!factor(role, p.sigma, nullptr)) { MPCQ_SET_XST(MPCQ_STATUS_FACTOR_FAILED); break; }
+            kinv_form(role, kv);
+            STAMP(2);
+            bool refactor = false;
+            // one ADMM iteration: ph_rhs, barrier A, the product, ph_recover (barrier B), update
+            auto ki_iter = [&](auto mode_tag, const RhsOps& ops, double (&dyv)[3], double& dxf_, double& dxX_,
+                               double (&cvp)[CK_COUNT]) __attribute__((always_inline)) {
+              constexpr bool DELTA = decltype(mode_tag)::value == 1;
+              lds_d* const rs = ki_rsum(iter & 1);
+              if constexpr (H) {
+                STAMP(15);
+                sync_all();  // A
+                STAMP(3);
+                kinv_mv(role, kv, rs);
+                if constexpr (DELTA) ck_all(cvp);
+                STAMP(6);
+                sync_all();  // B
+                STAMP(7);
+              } else {
+                double uf, beta, sf, sX, ax[3];
+                ph_rhs(true, &ops, kNoW, 0.0, 0.0, uf, beta, rs);
+                STAMP(15);
+                sync_all();  // A: r = bo + na summed
+                STAMP(3);
+                kinv_mv(role, kv, rs);
+                STAMP(6);
+                if constexpr (DELTA) ck_all(cvp);
+                ph_recover(&ops, ri[0], uf, beta, sf, sX, ax);  // (B inside: the partial products)
+                // every read of this buffer preceded B; it is summed into again two iterations on
+                if (cl) rs[12 * k + ph] = 0.0;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                  const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
+                  const double tt = zr + ri[j] * y[j];
+                  const double zn = fmin(fmax(tt, lo_of(j)), hi_of(j));  // osqp project
+                  const double d = rr[j] * (zr - zn);
+                  if constexpr (DELTA) dyv[j] = d;
+                  y[j] = y[j] + d;
+                  z[j] = zn;
+                }
+                const double nxf = p.alpha * sf + (1.0 - p.alpha) * xf;
+                const double nxX = p.alpha * sX + (1.0 - p.alpha) * xX;
+                if constexpr (DELTA) { dxf_ = nxf - xf; dxX_ = nxX - xX; }
+                xf = nxf;
+                xX = nxX;
+              }
+              STAMP(10);
+            };
+            while (iter <= p.max_iter) {
+              int until = p.max_iter - iter + 1;
+              if (chk_on && to_check < until) until = to_check;
+              if (adp_on && to_adapt < until) until = to_adapt;
+              double dyv[3], dxf_, dxX_;
+              RhsOps ops;
+              if constexpr (!H) load_rhs_ops(ops);
+              double cvp[CK_COUNT];
+#pragma nounroll
+              for (int r_ = 1; r_ < until; ++r_, ++iter)
+                ki_iter(std::integral_constant<int, 0>{}, ops, dyv, dxf_, dxX_, cvp);
+              ki_iter(std::integral_constant<int, 1>{}, ops, dyv, dxf_, dxX_, cvp);
+              const bool can_check = chk_on && (to_check -= until) == 0;
+              if (can_check) to_check = p.check_termination;
+              const bool adapt = adp_on && (to_adapt -= until) == 0;
+              if (adapt) to_adapt = p.adaptive_rho_interval;
+              last_checked = can_check;
+              if constexpr (H) {
+                sync_all();  // infeas_cheap's publication
+                sync_all();  // update_info: the stage waves' residual terms
+                info_combine(std::true_type{}, cvp, sh.red, 32);
+                sync_all();
+              } else {
+                infeas_cheap(dyv, dxf_, dxX_, cvp);
+                update_info(std::true_type{}, cvp);
+              }
+              if (inf_need) infeas_products(role, dxf_, dxX_, cvp);
+              // the checks published into the summed right-hand sides' buffers: zero them again,
+              // and a barrier before the next iteration sums into them
+              if constexpr (!H) {
+                if (cl) { ki_rsum(0)[12 * k + ph] = 0.0; ki_rsum(1)[12 * k + ph] = 0.0; }
+              }
+              sync_all();
+              if (!(isfinite(pri_res) && isfinite(dua_res))) { MPCQ_SET_XST(MPCQ_STATUS_NONFINITE); break; }
+              if (can_check) {
+                if (converged(1.0)) { MPCQ_SET_XST(MPCQ_STATUS_SOLVED); break; }
+                if (inf_bits & 1) { MPCQ_SET_XST(MPCQ_STATUS_PRIMAL_INFEASIBLE); break; }
+                if (inf_bits & 2) { MPCQ_SET_XST(MPCQ_STATUS_DUAL_INFEASIBLE); break; }
+              }
+              if (adapt) {
+                double rn = rho_s * sqrt(s_pri / (s_dua + kDivTol));
+                rn = fmin(fmax(rn, kRhoMin), kRhoMax);
+                if (rn > rho_s * p.adaptive_rho_tolerance || rn < rho_s / p.adaptive_rho_tolerance) {
+                  rho_s = rn;
+                  if constexpr (!H) {
+                    set_rho();
+                    zc_store();
+                  }
+                  refactor = true;
+                  ++n_upd;
+                  ++iter;
+                  sync_all();
+                  break;
+                }
+              }
+              STAMP(11);
+              ++iter;
+            }
+            if (!refactor) break;
+          }
+          sync_all();  // thread 0's exit status (kXstLds)
+          if constexpr (!H) status = sh.flag[4];
+        };
+        static_assert(!KI || kXstLds<N>, "the explicit inverse reads the exit status from LDS");
+        if (wvu() >= NW) {  // the helpers: nothing of theirs is an output
+          kinv_admm(std::true_type{});
+          return;
+        }
+        kinv_admm(std::false_type{});
+      } else {
       // the bounds are re-derived where used (lo_of / hi_of: a select on the lane's
       // class and its row scaling in the fused path) rather than held in 6 registers
       for (;;) {
@@ -2564,7 +3000,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         const uint64_t ft0_ = __builtin_amdgcn_s_memtime();
 #endif
 #pragma nounroll
-        for (int rep_ = 0; rep_ < MPCQ_REP_FACTOR; ++rep_) fac_ok = factor(p.sigma, nullptr);  // > 1: timing only
+        for (int rep_ = 0; rep_ < MPCQ_REP_FACTOR; ++rep_) fac_ok = factor(std::false_type{}, p.sigma, nullptr);  // > 1: timing only
 #ifdef MPCQ_FACTIME
         fac_cycles += __builtin_amdgcn_s_memtime() - ft0_;
 #endif
@@ -2649,7 +3085,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
           // live (osqp's update_info after the loop when the last iteration was unchecked)
           infeas_cheap(dyv, dxf_, dxX_, cvp);
           update_info(std::true_type{}, cvp);
-          if (inf_need) infeas_products(dxf_, dxX_, cvp);
+          if (inf_need) infeas_products(std::false_type{}, dxf_, dxX_, cvp);
           if (!(isfinite(pri_res) && isfinite(dua_res))) { MPCQ_SET_XST(MPCQ_STATUS_NONFINITE); break; }
           if (can_check) {  // osqp check_termination
             if (converged(1.0)) { MPCQ_SET_XST(MPCQ_STATUS_SOLVED); break; }
@@ -2679,6 +3115,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
         sync_all();  // thread 0's exit status
         status = sh.flag[4];
       }
+      }  // !KI
       if constexpr (kXstRe<N>) {  // the exit's reason, as the loop tested it (kXstRe)
         if (sh.flag[2] != 0) status = MPCQ_STATUS_FACTOR_FAILED;
         else if (iter <= p.max_iter) {
@@ -2774,7 +3211,7 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
               if (same) break;
             }
             ++pol_rounds;
-            if (!factor(p.sigma, prho)) break;
+            if (!factor(std::false_type{}, p.sigma, prho)) break;
 #pragma unroll
             for (int j = 0; j < 3; ++j) { rr[j] = prho[j]; ri[j] = act[j] ? 1.0 / kPolishRho : 0.0; }
             // one proximal multiplier step from the ADMM point (x, y on the active rows),
@@ -2927,16 +3364,16 @@ __global__ __launch_bounds__(16 * kRows<N>, 2) void engine_kernel(mpcq_params p,
 template <int N>
 hipError_t launch_t(bool fused, bool solve, const mpcq_params& p, const LaunchArgs& a,
                     hipStream_t s) {
-  const dim3 grid((unsigned)a.batch), block(16 * kRows<N>);
+  const dim3 grid((unsigned)a.batch), block(16 * kRows<N>), block2(16 * kRows<N> * (kKinv<N> ? 2 : 1));
   if (kBig<N> && solve && !a.work) return hipErrorInvalidValue;  // the caller sizes it with work_doubles(N)
   // polish lives in its own instantiation: the production kernel's code (and its
   // register allocation in the ADMM loop) does not carry it
   const bool pol = p.polish != 0;
   if (!solve) hipLaunchKernelGGL((engine_kernel<N, true, false, false>), grid, block, 0, s, p, a);
   else if (fused && pol) hipLaunchKernelGGL((engine_kernel<N, true, true, true>), grid, block, 0, s, p, a);
-  else if (fused) hipLaunchKernelGGL((engine_kernel<N, true, true, false>), grid, block, 0, s, p, a);
+  else if (fused) hipLaunchKernelGGL((engine_kernel<N, true, true, false>), grid, block2, 0, s, p, a);
   else if (pol) hipLaunchKernelGGL((engine_kernel<N, false, true, true>), grid, block, 0, s, p, a);
-  else hipLaunchKernelGGL((engine_kernel<N, false, true, false>), grid, block, 0, s, p, a);
+  else hipLaunchKernelGGL((engine_kernel<N, false, true, false>), grid, block2, 0, s, p, a);
   return hipGetLastError();
 }
 
@@ -2949,6 +3386,7 @@ hipError_t launch_t(bool fused, bool solve, const mpcq_params& p, const LaunchAr
 #endif
 static_assert(MPCQ_ENGINE_N >= 4 && kRows<MPCQ_ENGINE_N> <= 64, "horizons 4..64 (1024 threads at most)");
 static_assert(sizeof(Smem<MPCQ_ENGINE_N>) <= 160 * 1024, "Smem<N> exceeds the CU's LDS");
+static_assert(sizeof(Smem<MPCQ_ENGINE_N, kKinv<MPCQ_ENGINE_N>>) <= 160 * 1024, "Smem<N, KI> exceeds the CU's LDS");
 static_assert(Work<MPCQ_ENGINE_N>::SIZE == (kBig<MPCQ_ENGINE_N> ? work_doubles(MPCQ_ENGINE_N) : 72 + Work<MPCQ_ENGINE_N>::ZERO),
               "work_doubles(N) (mpcq_internal.h) and Work<N> disagree");
 static_assert(kRows<MPCQ_ENGINE_N> > 16 || sizeof(Smem<MPCQ_ENGINE_N>) <= 80 * 1024,

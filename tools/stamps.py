@@ -23,6 +23,11 @@ NAMES[3] = "iter:rhs barrier wait"
 # the cyclic-reduction build (kCR horizons): bucket 3 is ph_rhs + its barrier, 15 the
 # reduction of b + its barrier, 12 the outward sweep + the barrier after it, 7 the
 # back-substitution of the odd stages + ph_recover's barrier
+# the explicit-inverse build (kKI, N = 16): bucket 6 is the product, 7 the wait at its barrier
+NAMES_KI = list(NAMES)
+NAMES_KI[6] = "iter:Z r product (own share)"
+NAMES_KI[7] = "iter:product barrier wait"
+NAMES_KI[2] = "factor + Z formation"
 NAMES_CR = list(NAMES[:15]) + ["cr:reduce b + barrier"]
 NAMES_CR[3] = "iter:w,b,u,beta + barrier"
 NAMES_CR[7] = "cr:odd stages + barrier"
@@ -34,6 +39,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--N", type=int, default=16)
     ap.add_argument("--cr", action="store_true", help="label the buckets of the cyclic-reduction build")
+    ap.add_argument("--ki", action="store_true", help="label the buckets of the explicit-inverse build (N = 16)")
     ap.add_argument("--copies", type=int, default=-1,
                     help=">= 0: every instance a copy of this instance of the C2 batch (seed 2)")
     a = ap.parse_args()
@@ -58,7 +64,7 @@ def main():
     torch.cuda.synchronize()
     S = stamps.cpu().numpy().astype(np.float64)
     its = it.cpu().numpy()
-    names = NAMES_CR if a.cr else NAMES
+    names = NAMES_CR if a.cr else (NAMES_KI if a.ki else NAMES)
     tot = S[:, :13].sum(axis=1) + S[:, 15]
     print(f"batch {a.batch} N={a.N}: iters median {np.median(its)} max {its.max()}; "
           f"kernel ms (event) {eng.last_kernel_ms()[1]:.2f}")

@@ -578,15 +578,26 @@ __host__ __device__ constexpr int SLOT(int q) { return GS * q + (q > N / 2 ? kSl
 // Horizons beyond 32 stages do not fit a CU's LDS (N = 48: 236 KB): S^{-1}, F W and
 // R^{-1} Q move to a per-instance global workspace (LaunchArgs::work, work_doubles(N)
 // doubles per instance, L2-resident), the rest stays in LDS (N = 48: 140 KB).
+// Occupancy experiment (round 5, -DMPCQ_OCC16=3 or 4): the 16-stage kernel with the
+// beyond-32-stage layout (S^{-1}, R^{-1} Q and the scaled constraint values in the global
+// workspace, the split sweep) and __launch_bounds__(..., 3 / 4), so that three or four
+// instances share a CU (LDS 39.5 KB; 168 / 128 VGPRs).  Not the default.
+#ifdef MPCQ_OCC16
 template <int N>
-constexpr bool kBig = N > 32;
+constexpr int kOcc = N == 16 ? MPCQ_OCC16 : 2;
+#else
+template <int N>
+constexpr int kOcc = 2;
+#endif
+template <int N>
+constexpr bool kBig = N > 32 || kOcc<N> > 2;
 // F W stays in LDS at every N (the ADMM loop reads it every iteration: from L2 at
 // N = 48 it cost the right-hand-side phase ~14 k cycles per iteration, r03d
 // stamps); beyond 49 stages the scaled constraint values (126 N - 18 doubles) leave
 // LDS instead (N = 64: 197 KB with them, 133 KB without); the engine reads them
 // through the same accessors, the stage-parallel phases from L2.
 template <int N>
-constexpr bool kAbG = N > 49;
+constexpr bool kAbG = N > 49 || kOcc<N> > 2;
 // Beyond 48 stages (13-16 waves: 128 VGPRs) the F_k row is read from the workspace in
 // the loop and the z update's constants are batch-loaded from private memory instead
 // of being held; from 33 to 48 stages (168 VGPRs) holding them is faster.  Measured at
@@ -622,7 +633,7 @@ template <int N> constexpr bool kLagOut = N <= 48;
 // Up to 32 stages, where the LDS has the 24 N doubles (N = 16: 80,048 B, still two
 // instances per CU).
 template <int N, bool KI = false>
-constexpr int kFWS = (N <= 32 && !KI) ? 96 : 72;  // (kKI: the LDS goes to Z's columns)
+constexpr int kFWS = (!kBig<N> && !KI) ? 96 : 72;  // (kKI: the LDS goes to Z's columns)
 // Up to 16 stages the ADMM loop's exit status goes through LDS (Smem::flag[4]) instead of
 // a register carried across the loop: the N = 16 kernel then spills 27 instead of 43
 // VGPRs (scratch 256 -> 224 B per lane) and its C2 HBM traffic falls 127 -> 88 MB per
@@ -766,7 +777,7 @@ struct Prologue {
 // !FUSED: solve the given (Ax, l, u).  SOLVE=false: formulation only.
 
 template <int N, bool FUSED, bool SOLVE, bool POLISH>
-__global__ __launch_bounds__((16 * kRows<N> * (kKI<N, SOLVE, POLISH> ? 2 : 1)), (kKI<N, SOLVE, POLISH> ? 1 : 2))
+__global__ __launch_bounds__((16 * kRows<N> * (kKI<N, SOLVE, POLISH> ? 2 : 1)), (kKI<N, SOLVE, POLISH> ? 1 : kOcc<N>))
 void engine_kernel(mpcq_params p, LaunchArgs a) {
   // KI: the explicit inverse (kKI): twice the threads, waves NW.. are the helpers
   constexpr bool KI = kKI<N, SOLVE, POLISH>;

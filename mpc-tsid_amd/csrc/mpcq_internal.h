@@ -40,8 +40,20 @@ struct LaunchArgs {
 // a zero block (72), beyond 49 stages the scaled constraint values (126 N - 18,
 // rounded up to even), beyond 48 every lane's row of F_k (12 x 16 x the stage rows, N
 // rounded up to 4); the F W block stays reserved (F W lives in LDS since round 3)
+// (-DMPCQ_OCC16=3/4, an experiment: the 16-stage kernel in the beyond-32 layout, its
+// scaled constraint values in the workspace too -- mpcq_engine.hip kOcc)
+#if defined(MPCQ_OCC3) && !defined(MPCQ_OCC16)
+#define MPCQ_OCC16 3
+#elif defined(MPCQ_OCC4) && !defined(MPCQ_OCC16)
+#define MPCQ_OCC16 4
+#endif
+#ifdef MPCQ_OCC16
+constexpr bool work_occ16(int N) { return N == 16 && MPCQ_OCC16 > 2; }
+#else
+constexpr bool work_occ16(int) { return false; }
+#endif
 constexpr int64_t work_doubles(int N) {
-  return N > 32 ? 288 + (int64_t)N * (144 + 72 + 36) + 2 + 72 + (N > 49 ? ((126 * N - 18 + 1) & ~1) : 0) +
+  return (N > 32 || work_occ16(N)) ? 288 + (int64_t)N * (144 + 72 + 36) + 2 + 72 + ((N > 49 || work_occ16(N)) ? ((126 * N - 18 + 1) & ~1) : 0) +
                       (N > 48 ? (int64_t)12 * 16 * ((N + 3) & ~3) : 0)
                 : 0;
 }

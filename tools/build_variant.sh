@@ -24,7 +24,9 @@ OBJS=""
 HX=""
 for n in $HS; do OBJS="$OBJS $OUT/$NAME/e$n.o"; HX="$HX X($n)"; done
 printf '#include "mpcq_internal.h"\n#undef MPCQ_HORIZONS\n#define MPCQ_HORIZONS(X) %s\n#include "mpcq_dispatch.cpp"\n' "$HX" > $OUT/$NAME/dispatch.cpp
-/opt/rocm/bin/hipcc $F -I$R/include -c -o $OUT/$NAME/dispatch.o $OUT/$NAME/dispatch.cpp
+/opt/rocm/bin/hipcc $F "$@" -I$R/include -c -o $OUT/$NAME/dispatch.o $OUT/$NAME/dispatch.cpp
+# the C ABI with the variant's flags too (a layout switch changes work_doubles)
+/opt/rocm/bin/hipcc $F "$@" -I$R/include -c -o $OUT/$NAME/api.o $C/mpcq_api.cpp
 /opt/rocm/bin/hipcc $F -shared -o $OUT/libmpcq_$NAME.so $OBJS $C/build/mpcq_planner.o $C/build/mpcq_session.o \
-  $C/build/mpcq_api.o $C/build/mpcq_build.o $OUT/$NAME/dispatch.o
+  $OUT/$NAME/api.o $C/build/mpcq_build.o $OUT/$NAME/dispatch.o
 echo "built $OUT/libmpcq_$NAME.so"

@@ -377,8 +377,29 @@ __device__ __forceinline__ void gj_fmac(double (&c)[12], const double (&R)[12], 
 // FOLD = false (beyond 32 stages): the DPP move + FMA form -- the folded blocks hold all
 // their operands at once, which the 168 / 128-VGPR budgets there pay for in spills inside
 // the ADMM loop (N = 48: 6 -> 15 scratch reloads per iteration in the gfx950 assembly)
+// Lazy pivot rows (round 5): the pivot row is not normalised when it is used -- its lane's
+// multiplier is 0, so its row stays p and its diagonal becomes 1 -- and each row is scaled
+// by its own pivot's 1/d once, after the twelfth step.  A row that has been a pivot is then
+// d times the textbook (normalised) row; every later update of it is linear in the row, so
+// it stays d times the textbook row, and the final scaling gives the same inverse.  It saves
+// the selects that gave the pivot lane a zero base (22 v_cndmask_b32 per pivot, about 40 %
+// of the Gauss-Jordan instructions) for 12 multiplies at the end; the rounding differs from
+// the normalised form in the last bits.  Up to 32 stages (FOLD); beyond, the normalised
+// form stays: the lazy one measured 12-14 % fewer factorisation cycles (N = 16 84.8 k ->
+// 74.1 k, N = 32 124 k -> 108 k, profiles/r05h_factime*) with the statuses and iterations
+// of the oracle kept, but at N = 48 its (2-3x larger, ~1e-12) first-solve rounding grew to
+// 2.1e-7 after five warm-started ticks (8.1e-8 normalised; tools/drift.py,
+// profiles/r05j_drift_*).  -DMPCQ_GJ_NORM: the normalised form everywhere.
+#ifdef MPCQ_GJ_NORM
+template <bool FOLD>
+constexpr bool kGjLazy = false;
+#else
+template <bool FOLD>
+constexpr bool kGjLazy = FOLD;
+#endif
 template <int PV, bool FOLD>
-__device__ __forceinline__ void gj_step(double (&R)[12], int me, bool& ok) {
+__device__ __forceinline__ void gj_step(double (&R)[12], int me, bool& ok, double& sc) {
+  constexpr bool LAZY = kGjLazy<FOLD>;
   const double d = rbc<LN(PV)>(R[PV]);
 #ifdef MPCQ_DEBUG_PIVOT
   if (!(d > 0.0) && me == PV) printf("pivot fail blk %d thr %d PV %d d %g\n", (int)blockIdx.x, (int)threadIdx.x, PV, d);
@@ -391,14 +412,15 @@ __device__ __forceinline__ void gj_step(double (&R)[12], int me, bool& ok) {
   id = fma(id, e_, id);
   e_ = fma(-d, id, 1.0);
   id = fma(id, e_, id);
-  // one multiplier per row: the pivot row becomes p / d, every other row
-  // R - (R[PV] / d) p, so each entry is a single FMA on the broadcast pivot row
+  // one multiplier per row: every other row R - (R[PV] / d) p, so each entry is a single
+  // FMA on the broadcast pivot row; the pivot row itself: p / d (normalised form) or p
+  // (lazy: multiplier 0, scaled by sc = 1/d at the end)
   const bool isp = me == PV;
-  const double a = isp ? id : -(R[PV] * id);
+  const double a = isp ? (LAZY ? 0.0 : id) : -(R[PV] * id);
   if constexpr (FOLD) {
     double c[12];
 #pragma unroll
-    for (int j = 0; j < 12; ++j) c[j] = isp ? 0.0 : R[j];
+    for (int j = 0; j < 12; ++j) c[j] = (isp && !LAZY) ? 0.0 : R[j];
     gj_fmac<PV>(c, R, a);
 #pragma unroll
     for (int j = 0; j < 12; ++j)
@@ -407,19 +429,29 @@ __device__ __forceinline__ void gj_step(double (&R)[12], int me, bool& ok) {
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
       if (j == PV) continue;
-      const double base = isp ? 0.0 : R[j];
+      const double base = (isp && !LAZY) ? 0.0 : R[j];
       R[j] = fma(a, rbc<LN(PV)>(R[j]), base);
     }
   }
-  R[PV] = a;
+  if constexpr (LAZY) {
+    R[PV] = isp ? 1.0 : a;
+    if (isp) sc = id;
+  } else {
+    R[PV] = a;
+  }
 }
 template <bool FOLD, int... P>
-__device__ __forceinline__ void gj_seq(double (&R)[12], int me, bool& ok, std::integer_sequence<int, P...>) {
-  (gj_step<P, FOLD>(R, me, ok), ...);
+__device__ __forceinline__ void gj_seq(double (&R)[12], int me, bool& ok, double& sc, std::integer_sequence<int, P...>) {
+  (gj_step<P, FOLD>(R, me, ok, sc), ...);
 }
 template <bool FOLD>
 __device__ __forceinline__ void gj12(double (&R)[12], int me, bool& ok) {
-  gj_seq<FOLD>(R, me, ok, std::make_integer_sequence<int, 12>{});
+  double sc = 1.0;
+  gj_seq<FOLD>(R, me, ok, sc, std::make_integer_sequence<int, 12>{});
+  if constexpr (kGjLazy<FOLD>) {
+#pragma unroll
+    for (int j = 0; j < 12; ++j) R[j] *= sc;
+  }
 }
 
 // Ro -= G C' for one 12x12 coupling block C held one row per column lane in

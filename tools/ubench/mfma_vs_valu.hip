@@ -66,17 +66,21 @@ __global__ void bench(const double* A, const double* B, double* out, unsigned lo
   for (int r = 0; r < 4; ++r) out[768 + 64 * r + l] = acc[r];
   // ---- four independent products (issue rate)
   d4 q0 = {0, 0, 0, 0}, q1 = q0, q2 = q0, q3 = q0;
+  double a1[4], a2[4], a3[4];  // distinct operands (no common subexpressions)
+  for (int s = 0; s < 4; ++s) { a1[s] = 2.0 * am[s]; a2[s] = 3.0 * am[s]; a3[s] = 4.0 * am[s]; }
+  asm volatile("" : "+v"(a1[0]), "+v"(a1[1]), "+v"(a1[2]), "+v"(a1[3]), "+v"(a2[0]), "+v"(a2[1]), "+v"(a2[2]),
+               "+v"(a2[3]), "+v"(a3[0]), "+v"(a3[1]), "+v"(a3[2]), "+v"(a3[3]));
   TIC
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     q0 = __builtin_amdgcn_mfma_f64_16x16x4f64(am[s], bm[s], q0, 0, 0, 0);
-    q1 = __builtin_amdgcn_mfma_f64_16x16x4f64(am[s], bm[s], q1, 0, 0, 0);
-    q2 = __builtin_amdgcn_mfma_f64_16x16x4f64(am[s], bm[s], q2, 0, 0, 0);
-    q3 = __builtin_amdgcn_mfma_f64_16x16x4f64(am[s], bm[s], q3, 0, 0, 0);
+    q1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s], bm[s], q1, 0, 0, 0);
+    q2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[s], bm[s], q2, 0, 0, 0);
+    q3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a3[s], bm[s], q3, 0, 0, 0);
   }
   asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
   TOC(2)
-  for (int r = 0; r < 4; ++r) out[1024 + 64 * r + l] = q0[r] + q1[r] - q2[r] - q3[r] + acc[r];
+  for (int r = 0; r < 4; ++r) out[1024 + 64 * r + l] = q0[r] + q1[r] + q2[r] - q3[r];  // (1 + 2 + 3 - 4) P = 2 P
   // ---- MFMA with the conversions: rows of 12 (lane ph) -> LDS -> MFMA maps -> D -> LDS -> rows
   double oc[12];
   TIC
@@ -117,6 +121,9 @@ __global__ void bench(const double* A, const double* B, double* out, unsigned lo
   for (int r = 0; r < 12; ++r) ch = col12(a, ch);
   TOC(5)
   out[2112 + l] = ch;
+  // ---- the timing brackets alone
+  TIC
+  TOC(6)
 }
 
 int main() {
@@ -137,26 +144,27 @@ int main() {
   hipMalloc(&dA, sizeof hA); hipMalloc(&dB, sizeof hB); hipMalloc(&dO, 4096 * 8); hipMalloc(&dC, 16 * 8);
   hipMemcpy(dA, hA, sizeof hA, hipMemcpyHostToDevice);
   hipMemcpy(dB, hB, sizeof hB, hipMemcpyHostToDevice);
-  unsigned long long best[6];
-  for (int i = 0; i < 6; ++i) best[i] = ~0ull;
+  unsigned long long best[7];
+  for (int i = 0; i < 7; ++i) best[i] = ~0ull;
   static double hO[4096];
   for (int rep = 0; rep < 20; ++rep) {
     hipLaunchKernelGGL(bench, dim3(1), dim3(64), 0, 0, dA, dB, dO, dC);
     unsigned long long c[16];
     hipMemcpy(c, dC, sizeof c, hipMemcpyDeviceToHost);
-    for (int i = 0; i < 6; ++i) best[i] = c[i] < best[i] ? c[i] : best[i];
+    for (int i = 0; i < 7; ++i) best[i] = c[i] < best[i] ? c[i] : best[i];
   }
   hipMemcpy(hO, dO, sizeof hO, hipMemcpyDeviceToHost);
-  int bad_v = 0, bad_m = 0, bad_c = 0;
+  int bad_v = 0, bad_m = 0, bad_c = 0, bad_4 = 0;
   for (int r = 0; r < 12; ++r)
     for (int c = 0; c < 12; ++c) {
       const double e = ref[12 * r + c];
       bad_v += fabs(hO[64 * c + r] - e) > 1e-12;                      // VALU: column c in out[64 c + lane r]
       bad_m += fabs(hO[768 + 64 * (r >> 2) + c + 16 * (r & 3)] - e) > 1e-12;  // D row r: reg r>>2, lane c + 16 (r&3)
       bad_c += fabs(hO[1280 + 64 * c + r] - e) > 1e-12;
+      bad_4 += fabs(hO[1024 + 64 * (r >> 2) + c + 16 * (r & 3)] - 2.0 * e) > 1e-11;
     }
-  printf("check: valu %d, mfma %d, mfma+conversion %d wrong of 144\n", bad_v, bad_m, bad_c);
-  printf("12x12x12 product, one wave, s_memtime cycles (best of 20):\n");
+  printf("check: valu %d, mfma %d, mfma4 %d, mfma+conversion %d wrong of 144\n", bad_v, bad_m, bad_4, bad_c);
+  printf("12x12x12 product, one wave, s_memtime cycles (best of 20; the brackets alone: %llu, included below)\n", best[6]);
   printf("  valu      4 products (one per 16-lane row), 144 v_fmac_f64_dpp : %llu (%.1f per product)\n", best[0],
          best[0] / 4.0);
   printf("  mfma      1 product, 4 dependent 16x16x4 MFMAs (operands in MFMA maps): %llu\n", best[1]);
@@ -164,5 +172,5 @@ int main() {
   printf("  mfma+cv   1 product with row<->MFMA layout conversions through LDS: %llu\n", best[3]);
   printf("  mfma_dep  16 dependent MFMAs: %llu (%.1f per MFMA)\n", best[4], best[4] / 16.0);
   printf("  valu_dep  144 dependent v_fmac_f64_dpp: %llu (%.2f per instruction)\n", best[5], best[5] / 144.0);
-  return bad_v || bad_m || bad_c;
+  return bad_v || bad_m || bad_c || bad_4;
 }

@@ -264,19 +264,27 @@ __device__ __forceinline__ double pair_sum32(double v) {
   const double a1 = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
   return a0 + a1;
 }
+// max(a, b) as the hardware instruction, for operands the compiler cannot prove canonical
+// (DPP / permlane moves, LDS loads): C's fmax would canonicalize each of them first (see
+// clamp_hw); the engine's values are never signalling NaNs
+__device__ __forceinline__ double fmax_hw(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ double row_pair_max(double v) {
   const long long b = __double_as_longlong(v);
   const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
   const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
-  return fmax(__longlong_as_double(((long long)hi[0] << 32) | lo[0]),
-              __longlong_as_double(((long long)hi[1] << 32) | lo[1]));
+  return fmax_hw(__longlong_as_double(((long long)hi[0] << 32) | lo[0]),
+                 __longlong_as_double(((long long)hi[1] << 32) | lo[1]));
 }
 __device__ __forceinline__ double pair_max(double v) {
   const long long b = __double_as_longlong(v);
   const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
   const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
-  return fmax(__longlong_as_double(((long long)hi[0] << 32) | lo[0]),
-              __longlong_as_double(((long long)hi[1] << 32) | lo[1]));
+  return fmax_hw(__longlong_as_double(((long long)hi[0] << 32) | lo[0]),
+                 __longlong_as_double(((long long)hi[1] << 32) | lo[1]));
 }
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -304,6 +312,16 @@ __device__ __forceinline__ double uni(double v) {
   const int lo = __builtin_amdgcn_readfirstlane((int)bits);
   const int hi = __builtin_amdgcn_readfirstlane((int)(bits >> 32));
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// min(max(v, lo), hi) as the two hardware instructions.  C's fmax / fmin on values the
+// compiler cannot prove canonical (loads, held registers) make it canonicalize each operand
+// first (v_max_f64 x, x: IEEE mode quiets a signalling NaN), one extra FP64 instruction per
+// bound and use; the engine's values are never signalling NaNs, and for every other input
+// (quiet NaNs included: maxNum / minNum) the result is the same.
+__device__ __forceinline__ double clamp_hw(double v, double lo, double hi) {
+  double r;
+  asm("v_max_f64 %0, %1, %2\n\tv_min_f64 %0, %0, %3" : "=&v"(r) : "v"(v), "v"(lo), "v"(hi));
+  return r;
 }
 __device__ __forceinline__ double sel3(int i, double a0, double a1, double a2) {
   return i == 0 ? a0 : (i == 1 ? a1 : a2);
@@ -1556,11 +1574,11 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
     auto tstep = [](auto ctrl, double a, double b, bool hi) __attribute__((always_inline)) {
       constexpr int C = decltype(ctrl)::value;
       const double mine = hi ? b : a, send = hi ? a : b;
-      return fmax(mine, dppd<C>(send));
+      return fmax_hw(mine, dppd<C>(send));
     };
     auto sstep = [](auto ctrl, double a) __attribute__((always_inline)) {
       constexpr int C = decltype(ctrl)::value;
-      return fmax(a, dppd<C>(a));
+      return fmax_hw(a, dppd<C>(a));
     };
     using kMirror = std::integral_constant<int, 0x140>;   // row_mirror (s ^ 15)
     using kHalfMir = std::integral_constant<int, 0x141>;  // row_half_mirror (s ^ 7)
@@ -1823,7 +1841,7 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
       const int e = s < 6 ? s : 0;  // slots 16..21 are all maxima (0 / 2 / 3 from infeas_cheap)
       double v = sh.red[16 + e];
 #pragma unroll
-      for (int w = 1; w < NW; ++w) v = fmax(v, sh.red[32 * w + 16 + e]);
+      for (int w = 1; w < NW; ++w) v = fmax_hw(v, sh.red[32 * w + 16 + e]);
       const double ndy = rbc<0>(v), ndx = rbc<2>(v);  // (the cheap maxima, kept in slots 0 / 2)
       const double naty_ = rbc<1>(v), vu_ = rbc<4>(v), vl_ = rbc<5>(v);
       double epi0, edi0;
@@ -1902,7 +1920,7 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
       {
         double v = D[s];
 #pragma unroll
-        for (int w = 1; w < NW; ++w) v = fmax(v, D[DS * w + s]);
+        for (int w = 1; w < NW; ++w) v = fmax_hw(v, D[DS * w + s]);
         qv[0] = rbc<0>(v); qv[1] = rbc<2>(v); qv[2] = rbc<4>(v);
         qv[3] = rbc<8>(v); qv[4] = rbc<10>(v); qv[5] = rbc<12>(v);
         qv[6] = rbc<1>(v); qv[7] = rbc<3>(v); qv[8] = rbc<5>(v);
@@ -1925,7 +1943,7 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
 #pragma unroll
         for (int w = 1; w < NW; ++w) {
           const double t2 = D[DS * w + 16 + e];
-          v = s == 6 ? v + t2 : fmax(v, t2);
+          v = s == 6 ? v + t2 : fmax_hw(v, t2);
         }
         // kept in VGPRs (every lane holds the same values) and folded into one uniform
         // int at the end: SGPRs here would push loop-carried scalars into VGPR lanes
@@ -2122,13 +2140,33 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
       // xc = sigma x); polish with its own w and x terms.
       // the iteration-invariant LDS operands of ph_rhs (A_f column, F W column, the
       // state column's dynamics coefficients)
+      // (kColfFold, round 5) A_f's first coefficient masked by the force component: cf0m[j] =
+      // cf[0] on the lanes of component j (2: every other), else 0, so the component-dependent
+      // row broadcast of colF folds into v_fmac_f64_dpp.  With the right-hand-side phase's
+      // pointer laundering dropped (below) the phase lost ~40 instructions per wave and
+      // iteration: same box (profiles/r05p_*, r05q_*), N = 16 1.851-1.872 -> 1.788-1.791 us
+      // per iteration alone, 2.18-2.21 -> 2.134-2.142 at two per CU, N = 32 3.105-3.124 ->
+      // 2.966-2.982; C2 125.3 k -> 130.7 k QP/s.  The same terms in the same order (the
+      // compiler's own contraction of colF had rounded A_2 w_10 first, so the last bits of
+      // b_f differ from round 4's); statuses and iterations equal to the oracle's.  Up to 32
+      // stages: beyond, that last-bit change moved the N = 48 session loop's fifth tick
+      // 1.01e-7 from the oracle (its test allows 1e-7; r05r), and the loop reads its operands
+      // per iteration there anyway.  Dropping the checks' laundering as well was slower at
+      // N = 32 (3.06 us, r05q).
+      constexpr bool kColfFold = !KI && !BIG;
       struct RhsOps {
         double cf[10], fwc[12], cXd, cHd, cH6;
+        double cf0m[kColfFold ? 3 : 1];
       };
       auto load_rhs_ops = [&](RhsOps& o) __attribute__((always_inline)) {
         MPCQ_LANE_OFFS(true);  // (once per stretch of iterations)
 #pragma unroll
         for (int i = 0; i < 10; ++i) o.cf[i] = Ab[oF + i];
+        if constexpr (kColfFold) {
+          const int cs = cc == 0 ? 0 : (cc == 1 ? 1 : 2);
+#pragma unroll
+          for (int j = 0; j < 3; ++j) o.cf0m[j] = cs == j ? o.cf[0] : 0.0;
+        }
 #pragma unroll
         for (int psi = 0; psi < 12; ++psi) o.fwc[psi] = FWr[oFWcm + 6 * psi];
         o.cXd = Ab[oXd];
@@ -2142,7 +2180,10 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
       // bo / na stored apart -- the product then loads one value per column, not two and an add
       auto ph_rhs = [&](bool admm, const RhsOps* op, const double (&pw)[3], double xcf, double xcX, double& uf,
                         double& beta, lds_d* rsum = nullptr) __attribute__((always_inline)) {
-          launder_p();
+          // (up to 48 stages no launder_p here since round 5: the laundered base pointers
+          // cost ~40 instructions per iteration and the loop has no spill without them; beyond
+          // 48 stages, at 128 VGPRs, the iteration was 15.0 -> 16.9 us without, r05r)
+          if constexpr (kFrWork<N>) launder_p();
           RhsOps own_;
           if (!op) load_rhs_ops(own_);
           const RhsOps& o = op ? *op : own_;
@@ -2178,7 +2219,35 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
           }
           // the phase's arithmetic starts after this point, the loads before it
           asm volatile("" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]) : : "memory");
-          const double bf = colF_c(o.cf, w) + (admm ? p.sigma * xf : xcf);  // b_f = sigma x_f + A_f' w (- q, q = 0)
+          double colf;
+          if constexpr (kColfFold) {
+            // colF_c's six row-broadcast terms folded into v_fmac_f64_dpp (the masked terms
+            // add exact zeros); the quad-broadcast terms as there
+            double sA = -0.0, sB = -0.0;
+            asm("s_nop 1\n\t"
+                "v_fmac_f64_dpp %0, %2, %3 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+                "v_fmac_f64_dpp %1, %2, %4 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+                "v_fmac_f64_dpp %0, %2, %5 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+                "v_fmac_f64_dpp %1, %2, %6 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+                "v_fmac_f64_dpp %0, %2, %7 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+                "v_fmac_f64_dpp %0, %2, %8 row_newbcast:13 row_mask:0xf bank_mask:0xf"
+                : "+v"(sA), "+v"(sB)
+                : "v"(w[0]), "v"(o.cf0m[0]), "v"(o.cf[1]), "v"(o.cf0m[1]), "v"(o.cf[3]), "v"(o.cf0m[2]),
+                  "v"(o.cf[2]));
+            static_assert(LN(6) == 8 && LN(7) == 9 && LN(8) == 10 && LN(9) == 12 && LN(10) == 13 && LN(11) == 14,
+                          "the broadcast lanes above");
+            const double wf0 = qbc<0>(w[2]), wf1 = qbc<1>(w[2]), wf2 = qbc<2>(w[2]);
+            const double wf3 = qbc<3>(w[0]), wf4 = qbc<3>(w[1]);
+            const double* const A = o.cf;
+            sA += A[4] * w[1];
+            sB += A[5] * (cc == 1 ? wf2 : wf0);
+            sA += A[6] * (cc == 1 ? wf3 : wf1);
+            const double sC = (A[7] * wf2 + A[8] * wf3) + A[9] * wf4;
+            colf = (sA + sB) + m2 * sC;
+          } else {
+            colf = colF_c(o.cf, w);
+          }
+          const double bf = colf + (admm ? p.sigma * xf : xcf);  // b_f = sigma x_f + A_f' w (- q, q = 0)
           // u = F b_f (kept for the forces) and beta = R B u = (F W)' b_f (rows 6..11)
           if constexpr (kFrWork<N>) {
             uf = bdot_ln12(frg, bf, 0.0);
@@ -3088,7 +3157,7 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
           for (int j = 0; j < 3; ++j) {
             const double zr = p.alpha * ax[j] + (1.0 - p.alpha) * z[j];
             const double tt = zr + zri[j] * y[j];
-            const double zn = fmin(fmax(tt, zl[j]), zh[j]);  // osqp project: c_min(c_max(tt, l), u)
+            const double zn = clamp_hw(tt, zl[j], zh[j]);  // osqp project: c_min(c_max(tt, l), u)
             const double d = zrr[j] * (zr - zn);
             if constexpr (DELTA) dyv[j] = d;
             y[j] = y[j] + d;

@@ -692,13 +692,15 @@ constexpr int kFWS = (!kBig<N> && !KI) ? 96 : 72;  // (kKI: the LDS goes to Z's 
 // so the status stays a register there.
 template <int N>
 constexpr bool kXstLds = N <= 16;
-// Beyond 16 stages (round 5) the exit status is not carried at all: after the loop it is
+// From 17 to 48 stages (round 5) the exit status is not carried at all: after the loop it is
 // re-derived from what the loop leaves -- a failed factorisation sets sh.flag[2], and an
 // early exit stops with iter <= max_iter after the same tests, in the same order, on the
 // residuals and infeasibility bits that stay live after the loop anyway.  Carried in a
 // register, it was spilled and stored once per check segment at N = 32 (round 4).
+// Beyond 48 stages (128 VGPRs) the re-derivation cost the iteration 8 % (N = 64 15.2 -> 16.5
+// us alone, 19.7 -> 21.2 at 256 in flight, r05v): there the status is carried as in round 4.
 template <int N>
-constexpr bool kXstRe = !kXstLds<N>;
+constexpr bool kXstRe = !kXstLds<N> && N <= 48;
 // ---- The explicit state-system inverse (kKI, round 5) ------------------------------
 // At 16 stages the ADMM loop solves the state system K_s x = r (192 x 192, block
 // tridiagonal) with an explicit inverse Z = K_s^{-1} instead of the two-ended sweep: one

@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""Scan gfx950 assembly for DPP read-after-VALU-write hazards (and count the s_nop wait
+states that are not needed).
+
+    python asmpass/dpp_hazards.py <file.s> [--kernel SUBSTR]
+
+The rule (CDNA3 ISA, "manually inserted wait states"; LLVM's GCNHazardRecognizer): a DPP
+instruction that reads a VGPR as its DPP source (src0) needs two wait states after a VALU
+instruction that wrote that VGPR.  Every instruction issued in between counts as one wait
+state, `s_nop N` as N + 1.  The scan is linear within basic blocks (a label resets nothing:
+it assumes the worst, that the predecessor's last instructions immediately precede), which
+is conservative at block boundaries.  Exit status 1 if a hazard is found.
+"""
+import argparse
+import re
+import sys
+
+VREG = re.compile(r"v\[(\d+):(\d+)\]|v(\d+)\b")
+
+
+def regs(tok):
+    out = set()
+    for m in VREG.finditer(tok):
+        if m.group(1) is not None:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+        else:
+            out.add(int(m.group(3)))
+    return out
+
+
+def scan(lines):
+    """Yields (line_no, text, needed, available) for every DPP instruction, where
+    available = wait states since the last VALU write of its DPP source (capped at 3)."""
+    hist = []  # (wait states this instruction provides, VGPRs it wrote if VALU)
+    for no, raw in lines:
+        s = raw.split(";")[0].strip()
+        if not s or s.endswith(":") or s.startswith("."):
+            continue
+        op = s.split()[0]
+        args = s[len(op):]
+        if "_dpp" in op:
+            ops = [a.strip() for a in args.split(",")]
+            need = regs(ops[1].split()[0])  # src0, the DPP-read operand
+            ws = 0
+            avail = 3
+            for provided, wrote in reversed(hist[-4:]):
+                if wrote & need:
+                    avail = ws
+                    break
+                ws += provided
+                if ws >= 3:
+                    break
+            yield no, s, 2, avail
+        wrote = set()
+        if op.startswith("v_") and not op.startswith("v_readfirstlane") and not op.startswith("v_readlane") \
+                and not op.startswith("v_cmp"):
+            dst = args.split(",")[0].strip()
+            wrote = regs(dst)
+            if op.startswith("v_permlane"):  # both operands are written
+                wrote |= regs(args.split(",")[1])
+        provided = int(s.split()[1]) + 1 if op == "s_nop" else 1
+        hist.append((provided, wrote))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("asm")
+    ap.add_argument("--kernel", default="engine_kernel")
+    a = ap.parse_args()
+    text = open(a.asm).read().splitlines()
+    # the functions whose name contains the substring
+    funcs, cur = [], None
+    for i, l in enumerate(text):
+        m = re.match(r"^(_Z\S+):", l)
+        if m:
+            cur = m.group(1) if a.kernel in m.group(1) else None
+            if cur:
+                funcs.append((cur, []))
+        if cur and funcs:
+            funcs[-1][1].append((i + 1, l))
+        if l.startswith(".Lfunc_end"):
+            cur = None
+    bad = 0
+    for name, lines in funcs:
+        n = tight = 0
+        for no, s, need, avail in scan(lines):
+            n += 1
+            if avail < need:
+                bad += 1
+                print(f"HAZARD {name} line {no}: {s} (only {avail} wait states)")
+            elif avail == need:
+                tight += 1
+        print(f"{name}: {n} DPP instructions, {tight} with exactly the 2 wait states they need")
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

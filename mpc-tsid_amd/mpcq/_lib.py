@@ -257,10 +257,13 @@ def build_info() -> dict:
 
 def source_sha(csrc: str = CSRC) -> str:
     """The stamp the Makefile computes for the sources in ``csrc``: the first 16 hex
-    digits of sha256 over csrc/*.hip concatenated in name order."""
+    digits of sha256 over csrc/*.hip concatenated in name order, then the assembly
+    pass's scripts (Makefile ELIDE_PASS, in that order)."""
     import hashlib
     h = hashlib.sha256()
-    for name in sorted(n for n in os.listdir(csrc) if n.endswith(".hip")):
+    names = sorted(n for n in os.listdir(csrc) if n.endswith(".hip"))
+    names += [os.path.join("asmpass", n) for n in ("hipcc_elide.py", "nop_elide.py", "dpp_hazards.py")]
+    for name in names:
         with open(os.path.join(csrc, name), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]

@@ -13,8 +13,11 @@ OUT=$C/build/variants; mkdir -p $OUT/$NAME
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -I$C"
 HS=${VARIANT_HORIZONS:-16 32}  # the horizons compiled from the variant source
 J=0
+CC=/opt/rocm/bin/hipcc
+# through the production build's nop-elision pass (csrc/asmpass) unless NOELIDE=1
+if [ -z "$NOELIDE" ]; then CC="python3 $C/asmpass/hipcc_elide.py"; fi
 for n in $HS; do
-  /opt/rocm/bin/hipcc $F "$@" -DMPCQ_ENGINE_N=$n -c -o $OUT/$NAME/e$n.o -x hip $SRC &
+  $CC $F "$@" -DMPCQ_ENGINE_N=$n -c -o $OUT/$NAME/e$n.o -x hip $SRC &
   J=$((J + 1)); if [ $((J % 8)) -eq 0 ]; then wait; fi
 done
 wait

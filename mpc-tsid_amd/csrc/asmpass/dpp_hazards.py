@@ -4,9 +4,12 @@ states that are not needed).
 
     python asmpass/dpp_hazards.py <file.s> [--kernel SUBSTR]
 
-The rule (CDNA3 ISA, "manually inserted wait states"; LLVM's GCNHazardRecognizer): a DPP
-instruction that reads a VGPR as its DPP source (src0) needs two wait states after a VALU
-instruction that wrote that VGPR.  Every instruction issued in between counts as one wait
+The rule (CDNA3 ISA, "manually inserted wait states"): a DPP instruction that reads a VGPR
+needs two wait states after a VALU instruction that wrote that VGPR.  Checked here for
+every source operand (src0, the DPP-read one, and src1), but not for a v_fmac's tied
+accumulator: the engine's v_fmac_f64_dpp chains (bdot12 & co.) forward the accumulator from
+one instruction to the next with no wait state and are bit-exact against the oracle, so the
+hardware interlocks that operand (LLVM's checkDPPHazards would also count it).  Every instruction issued in between counts as one wait
 state, `s_nop N` as N + 1.  The scan is linear within basic blocks (a label resets nothing:
 it assumes the worst, that the predecessor's last instructions immediately precede), which
 is conservative at block boundaries.  Exit status 1 if a hazard is found.
@@ -40,7 +43,9 @@ def scan(lines):
         args = s[len(op):]
         if "_dpp" in op:
             ops = [a.strip() for a in args.split(",")]
-            need = regs(ops[1].split()[0])  # src0, the DPP-read operand
+            need = set()  # the VGPRs of every source (src0 is the DPP-read one)
+            for o in ops[1:]:
+                need |= regs(o.split()[0])
             ws = 0
             avail = 3
             for provided, wrote in reversed(hist[-4:]):

@@ -258,11 +258,12 @@ def build_info() -> dict:
 def source_sha(csrc: str = CSRC) -> str:
     """The stamp the Makefile computes for the sources in ``csrc``: the first 16 hex
     digits of sha256 over csrc/*.hip concatenated in name order, then the assembly
-    pass's scripts (Makefile ELIDE_PASS, in that order)."""
+    pass's scripts (Makefile ELIDE_PASS, in that order) and the Makefile."""
     import hashlib
     h = hashlib.sha256()
     names = sorted(n for n in os.listdir(csrc) if n.endswith(".hip"))
     names += [os.path.join("asmpass", n) for n in ("hipcc_elide.py", "nop_elide.py", "dpp_hazards.py")]
+    names.append("Makefile")
     for name in names:
         with open(os.path.join(csrc, name), "rb") as f:
             h.update(f.read())

@@ -93,3 +93,27 @@ def test_hipcc_wrapper_builds_and_leaves_no_hazard(tmp_path):
     assert r.returncode == 0, r.stderr
     assert "0 DPP hazards after" in r.stdout
     assert (tmp_path / "k.o").stat().st_size > 0
+
+
+def test_shipped_library_has_no_dpp_hazard():
+    """The library the GPU runs: its N = 16 and N = 32 engine code objects (the C2 / C3
+    kernels) extracted from .hip_fatbin, disassembled, and scanned as the build scanned
+    their assembly."""
+    import codeobj
+    so = os.path.join(REPO, "mpc-tsid_amd", "mpcq", "libmpcq.so")
+    if not os.path.exists(so):
+        pytest.skip("libmpcq.so not built")
+    seen = set()
+    for _, code in codeobj.extract(so):
+        ns = {n for n in (16, 32) if f"engine_kernelILi{n}E".encode() in code}  # (symbol names)
+        if not ns:
+            continue
+        funcs = codeobj.kernels(codeobj.disassemble(code))
+        seen |= ns
+        ndpp = 0
+        for name, lines in funcs.items():
+            found = list(dpp_hazards.scan(lines))
+            ndpp += len(found)
+            assert all(av >= need for _, _, need, av in found), name
+        assert ndpp > 1000  # the solve kernels' v_fmac_f64_dpp chains were scanned
+    assert seen == {16, 32}

@@ -23,7 +23,7 @@ KIND = {"ELb1ELb1ELb0EE": "fused solve (production)", "ELb1ELb1ELb1EE": "fused s
 
 def usage(N, extra=()):
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-function"]
-    if N in (16, 32):
+    if N != 40:
         flags += ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]  # as the Makefile
     cmd = ["/opt/rocm/bin/hipcc", *flags, *extra, f"-DMPCQ_ENGINE_N={N}", "-c", "-o", f"/tmp/ru_{N}.o",
            os.path.join(CSRC, "mpcq_engine.hip"), "-Rpass-analysis=kernel-resource-usage"]

@@ -128,8 +128,11 @@ int mpcq_pattern(int n_steps, int32_t* indptr, int32_t* indices);
 int mpcq_supported_horizons(int32_t* out, int cap);
 const char* mpcq_last_error(void);
 /* Build stamp of this library (no reference counterpart: provenance for profiles):
- * "src_sha256=<first 16 hex of sha256 over the csrc .hip files in name order> arch=gfx950".
- * bench.py drops a committed PMC figure whose stamp differs from the running library's. */
+ * "src_sha256=<16 hex> arch=gfx950", the hex the first 16 of sha256 over the csrc .hip files,
+ * the assembly pass, the Makefile, the headers, the .cpp units and the effective compiler
+ * flags (csrc/stamp.py); the stamps build appends "+stamps", an experiment variant
+ * "+exp:<name>:<hash>" (tools/build_variant.sh).  bench.py drops a committed PMC figure
+ * whose stamp differs from the running library's. */
 const char* mpcq_build_info(void);
 
 /* ---- context --------------------------------------------------------------

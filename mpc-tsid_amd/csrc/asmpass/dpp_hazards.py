@@ -12,7 +12,10 @@ one instruction to the next with no wait state and are bit-exact against the ora
 hardware interlocks that operand (LLVM's checkDPPHazards would also count it).  Every instruction issued in between counts as one wait
 state, `s_nop N` as N + 1.  The scan is linear within basic blocks (a label resets nothing:
 it assumes the worst, that the predecessor's last instructions immediately precede), which
-is conservative at block boundaries.  Exit status 1 if a hazard is found.
+is conservative at block boundaries.  The EXEC rule is checked the same way: a DPP
+instruction needs five wait states after a VALU write of EXEC (v_cmpx, or a VALU with EXEC
+as its destination).  v_permlane* and v_swap* write both of their operands.  Exit status 1
+if a hazard is found.
 """
 import argparse
 import re
@@ -31,10 +34,26 @@ def regs(tok):
     return out
 
 
+def valu_writes(op, args):
+    """(VGPRs, EXEC?) a VALU instruction writes; (set(), False) for anything else."""
+    if not op.startswith("v_") or op.startswith(("v_readfirstlane", "v_readlane")):
+        return set(), False
+    ops = args.split(",")
+    dst = ops[0].strip()
+    if op.startswith("v_cmp"):  # writes an SGPR pair / VCC, or EXEC (v_cmpx)
+        return set(), op.startswith("v_cmpx") or dst.startswith("exec")
+    wrote = regs(dst)
+    if op.startswith(("v_permlane", "v_swap")) and len(ops) > 1:  # both operands are written
+        wrote |= regs(ops[1])
+    return wrote, dst.startswith("exec")
+
+
 def scan(lines):
     """Yields (line_no, text, needed, available) for every DPP instruction, where
-    available = wait states since the last VALU write of its DPP source (capped at 3)."""
-    hist = []  # (wait states this instruction provides, VGPRs it wrote if VALU)
+    available = wait states since the last VALU write of its DPP source (capped at 3),
+    needed 2; or, where a VALU write of EXEC is fewer than five wait states back, that
+    count with needed 5."""
+    hist = []  # (wait states this instruction provides, VGPRs it wrote if VALU, EXEC written)
     for no, raw in lines:
         s = raw.split(";")[0].strip()
         if not s or s.endswith(":") or s.startswith("."):
@@ -48,23 +67,26 @@ def scan(lines):
                 need |= regs(o.split()[0])
             ws = 0
             avail = 3
-            for provided, wrote in reversed(hist[-4:]):
+            for provided, wrote, _ in reversed(hist[-4:]):
                 if wrote & need:
                     avail = ws
                     break
                 ws += provided
                 if ws >= 3:
                     break
-            yield no, s, 2, avail
-        wrote = set()
-        if op.startswith("v_") and not op.startswith("v_readfirstlane") and not op.startswith("v_readlane") \
-                and not op.startswith("v_cmp"):
-            dst = args.split(",")[0].strip()
-            wrote = regs(dst)
-            if op.startswith("v_permlane"):  # both operands are written
-                wrote |= regs(args.split(",")[1])
+            ws = 0
+            avail_x = 5
+            for provided, _, wx in reversed(hist[-6:]):
+                if wx:
+                    avail_x = ws
+                    break
+                ws += provided
+                if ws >= 5:
+                    break
+            yield (no, s, 5, avail_x) if avail_x < 5 else (no, s, 2, avail)
+        wrote, wexec = valu_writes(op, args)
         provided = int(s.split()[1]) + 1 if op == "s_nop" else 1
-        hist.append((provided, wrote))
+        hist.append((provided, wrote, wexec))
 
 
 def main():

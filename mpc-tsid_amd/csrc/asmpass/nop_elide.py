@@ -16,7 +16,9 @@ pass removes such a nop when all of the following hold (conservative on purpose)
     instruction of the region reads (covers the DPP-source rule, 2 wait states, and the
     transcendental-result rule, 1 wait state);
   - no VALU write of EXEC (v_cmpx) within the 5 instructions before it (DPP after an EXEC
-    write needs 5 wait states);
+    write needs 5 wait states); a label met in that walk ends it only where the program has
+    no VALU write of EXEC anywhere (a branch from elsewhere could otherwise arrive right
+    after one); else the nop stays;
   - the kernel has no MFMA (their result hazards are longer).
 After the pass, dpp_hazards.py re-scans the output and the build fails on any
 hazard.  Prints the count of nops kept and removed."""
@@ -24,7 +26,7 @@ import re
 import sys
 
 sys.path.insert(0, __import__("os").path.dirname(__file__))
-from dpp_hazards import regs  # noqa: E402
+from dpp_hazards import regs, valu_writes  # noqa: E402
 
 
 def instr(line):
@@ -35,14 +37,14 @@ def instr(line):
 
 
 def written(s):
+    """VGPRs a VALU instruction writes (v_permlane / v_swap: both operands)."""
     op = s.split()[0]
-    args = s[len(op):]
-    if not op.startswith("v_") or op.startswith(("v_readfirstlane", "v_readlane", "v_cmp")):
-        return set()
-    w = regs(args.split(",")[0])
-    if op.startswith("v_permlane"):
-        w |= regs(args.split(",")[1])
-    return w
+    return valu_writes(op, s[len(op):])[0]
+
+
+def writes_exec(s):
+    op = s.split()[0]
+    return valu_writes(op, s[len(op):])[1]
 
 
 def elide(lines):
@@ -50,6 +52,7 @@ def elide(lines):
         return lines, 0, sum(1 for l in lines if l.strip() == "s_nop 1")
     out = list(lines)
     removed = kept = 0
+    any_exec = any(instr(l) and writes_exec(instr(l)) for l in lines)
     i = 0
     n = len(lines)
     while i < n:
@@ -84,7 +87,7 @@ def elide(lines):
                 k -= 1
                 continue
             if raw.split(";")[0].strip().endswith(":"):  # a label (a branch target)
-                if seen < 2:
+                if seen < 2 or any_exec:
                     ok = False
                 break
             s = instr(lines[k])
@@ -92,7 +95,7 @@ def elide(lines):
                 k -= 1
                 continue
             op = s.split()[0]
-            if op.startswith("v_cmpx") or ("exec" in s.split(",")[0] and op.startswith("v_")):
+            if writes_exec(s):
                 ok = False
                 break
             if seen < 2:

@@ -256,18 +256,14 @@ def build_info() -> dict:
 
 
 def source_sha(csrc: str = CSRC) -> str:
-    """The stamp the Makefile computes for the sources in ``csrc``: the first 16 hex
-    digits of sha256 over csrc/*.hip concatenated in name order, then the assembly
-    pass's scripts (Makefile ELIDE_PASS, in that order) and the Makefile."""
-    import hashlib
-    h = hashlib.sha256()
-    names = sorted(n for n in os.listdir(csrc) if n.endswith(".hip"))
-    names += [os.path.join("asmpass", n) for n in ("hipcc_elide.py", "nop_elide.py", "dpp_hazards.py")]
-    names.append("Makefile")
-    for name in names:
-        with open(os.path.join(csrc, name), "rb") as f:
-            h.update(f.read())
-    return h.hexdigest()[:16]
+    """The stamp a default `make` gives the sources in ``csrc`` (csrc/stamp.py: sha256 over
+    the HIP sources, the assembly pass, the Makefile, the headers, the C++ units and the
+    Makefile's default flags; first 16 hex digits)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("mpcq_stamp", os.path.join(csrc, "stamp.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.stamp(csrc)
 
 
 def supported_horizons():

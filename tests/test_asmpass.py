@@ -33,6 +33,20 @@ def test_scan_flags_a_dpp_read_right_after_its_write():
     assert not hazards(["\tv_add_f64 v[6:7], v[6:7], v[8:9]", DPP])
 
 
+def test_scan_counts_both_operands_of_a_swap_and_the_exec_rule():
+    # v_swap_b32 writes both operands (as v_permlane): its second operand is a DPP source here
+    assert hazards(["\tv_swap_b32 v20, v2", DPP])
+    assert hazards(["\tv_swap_b32 v2, v20", DPP])
+    assert not hazards(["\tv_swap_b32 v20, v21", DPP])
+    # a VALU write of EXEC needs five wait states before a DPP instruction
+    cmpx = "\tv_cmpx_gt_f64_e32 vcc, v[6:7], v[8:9]"
+    mov = "\tv_mov_b32 v20, 0"
+    assert hazards([cmpx, mov, mov, DPP])
+    assert hazards([cmpx, mov, mov, mov, mov, DPP])
+    assert not hazards([cmpx, mov, mov, mov, mov, mov, DPP])
+    assert not hazards([cmpx, "\ts_nop 4", DPP])
+
+
 def test_elides_when_nothing_before_writes_the_inputs():
     src = block(["\tv_add_f64 v[2:3], v[6:7], v[8:9]", "\tv_mov_b32 v20, 0", "\tv_mov_b32 v21, 0"])
     out, removed, kept = nop_elide.elide(src)
@@ -54,6 +68,23 @@ def test_keeps_the_nop_when_needed_or_unsure(pre):
     out, removed, kept = nop_elide.elide(block(pre))
     assert (removed, kept) == (0, 1)
     assert out == block(pre)
+
+
+def test_a_swap_writing_the_dpp_source_keeps_the_nop():
+    pre = ["\tv_mov_b32 v20, 0", "\tv_swap_b32 v21, v3"]  # writes v3, half of the DPP source v[2:3]
+    out, removed, kept = nop_elide.elide(block(pre))
+    assert (removed, kept) == (0, 1)
+
+
+def test_a_label_is_no_stop_where_the_program_writes_exec_by_valu():
+    """A label two instructions back ends the walk only if nothing in the program writes EXEC
+    by VALU: a branch from elsewhere could land right after such a write."""
+    pre = ["\tv_mov_b32 v20, 0", ".LBB0_3:", "\tv_mov_b32 v21, 0", "\tv_mov_b32 v22, 0"]
+    out, removed, kept = nop_elide.elide(block(pre))
+    assert (removed, kept) == (1, 0)
+    elsewhere = ["\tv_cmpx_gt_f64_e32 vcc, v[6:7], v[8:9]", "\ts_cbranch_execz .LBB0_3"]
+    out, removed, kept = nop_elide.elide(elsewhere + block(pre))
+    assert (removed, kept) == (0, 1)
 
 
 def test_an_earlier_asm_region_is_read_as_instructions():

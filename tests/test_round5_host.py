@@ -88,3 +88,40 @@ def test_dist_fields_mark_rehearsals(bench):
     assert bench.dist_fields(8, "nccl", True, _FakeTorch(8)) == {"backend": "nccl", "distinct_devices": 8,
                                                                  "rehearsal": False}
     assert bench.dist_fields(1, "nccl", False, _FakeTorch(1))["backend"] is None
+
+
+def test_variant_and_stamps_builds_carry_their_own_stamp():
+    """an experiment variant (tools/build_variant.sh) and the stamps library link
+    their own mpcq_build.o, so their mpcq_build_info differs from the production build's and
+    bench.py's provenance gate drops production PMC figures for them."""
+    import subprocess
+    sys.path.insert(0, os.path.join(REPO, "mpc-tsid_amd"))
+    import mpcq
+    prod = mpcq.source_sha()
+    src = os.path.join(REPO, "mpc-tsid_amd", "csrc", "mpcq_engine.hip")
+
+    def vstamp(*flags):
+        r = subprocess.run(["bash", os.path.join(REPO, "tools", "build_variant.sh"), "--stamp-only", "ilp32", src,
+                            *flags], capture_output=True, text=True, timeout=60, check=True)
+        return r.stdout.strip()
+    a, b = vstamp(), vstamp("-DMPCQ_FR_HELD")
+    assert a.startswith(prod + "+exp:ilp32:") and b.startswith(prod + "+exp:ilp32:") and a != b
+    import bench
+    sys.path.insert(0, REPO)
+    entry = {"c3_N32_B1024": {"bytes_per_launch": 1.0, "tag": "rX", "engine_src_sha": prod}}
+    import json as _json
+    import tempfile
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        _json.dump(entry, f)
+    try:
+        assert bench.load_pmc("c3_N32_B1024", prod, f.name)["bytes_per_launch"] == 1.0
+        assert "stale" in bench.load_pmc("c3_N32_B1024", a, f.name)
+    finally:
+        os.unlink(f.name)
+    # the stamps library links mpcq_build_stamps.o (stamp + "+stamps"), not the production object
+    r = subprocess.run(["make", "-s", "-n", "-C", os.path.join(REPO, "mpc-tsid_amd", "csrc"), "../mpcq/libmpcq_stamps.so"],
+                       capture_output=True, text=True, timeout=120)
+    link = [ln for ln in r.stdout.splitlines() if "-shared" in ln and "libmpcq_stamps.so" in ln]
+    assert link and "mpcq_build_stamps.o" in link[-1] and "build/mpcq_build.o" not in link[-1]
+    assert any("+stamps" in ln for ln in r.stdout.splitlines()) or os.path.exists(
+        os.path.join(REPO, "mpc-tsid_amd", "csrc", "build", "mpcq_build_stamps.o"))

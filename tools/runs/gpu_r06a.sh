@@ -1,0 +1,16 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+# r06a: HEAD (stamp over every build input, asmpass v_swap / EXEC rules) -- the RCCL path at
+# world 1 with the stdout redirect (one JSON line, dist.backend nccl), the GPU suite, the C2
+# line with the reference25 reading
+O=gpurun_out
+MPCQ_FORCE_DIST=1 MPCQ_DIST_BACKEND=nccl WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 LOCAL_WORLD_SIZE=1 timeout -k 10 300 python -u bench.py --gpus 1 --steps 5 --warmup 1 --companion 0 --reference25 0 --cpu-sample 0 --certify 0 --restatement 64 --gather > $O/r06a_rccl_world1.json 2> $O/r06a_rccl_world1.err &&
+python3 -c "
+import json,sys
+L=[l for l in open('$O/r06a_rccl_world1.json').read().splitlines() if l.strip()]
+assert len(L)==1, L
+d=json.loads(L[0]); print('rccl world1 stdout lines', len(L), 'dist', d['dist'], 'value', d['value'])
+assert d['dist']['backend']=='nccl'
+" > $O/r06a_rccl_check.txt 2>&1 &&
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/r06a_pytest_gpu.log 2>&1 &&
+timeout -k 10 300 python -u bench.py > $O/r06a_bench_c2.json 2> $O/r06a_bench_c2.err

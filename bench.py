@@ -88,6 +88,11 @@ def parse():
                     help="1 (default, one GPU, reference headline): also time OSQP at MPC.py's settings with "
                          "adaptive_rho_interval 25 (the timing-derived interval of a PROFILING osqp build on a fast "
                          "host) on the same batch, with its own parity against the restatement at 25; 0 = skip")
+    ap.add_argument("--order-by-class", type=int, default=1,
+                    help="1 (default): MPCQ_FLAG_ORDER_BY_CLASS -- each launch dispatches the instances by the "
+                         "mean iteration count their gait class showed in the engine's earlier launches (the "
+                         "warm-up ones first), the most expensive first; a one-gait batch keeps index order. "
+                         "Scheduling only (results bit-identical); 0 = index order")
     ap.add_argument("--rho-interval", type=int, default=0,
                     help="override adaptive_rho_interval (0 = the library default)")
     ap.add_argument("--cpu-sample", type=float, default=1.5,
@@ -521,7 +526,8 @@ def main():
 
         def launch(x_ptr=0, y_ptr=0):
             eng.solve_device(per, xref_d.data_ptr(), fs_d.data_ptr(), f0_d.data_ptr(), st_d.data_ptr(),
-                             it_d.data_ptr(), x_ptr=x_ptr, y_ptr=y_ptr, info_ptr=info_d.data_ptr(), asynchronous=True)
+                             it_d.data_ptr(), x_ptr=x_ptr, y_ptr=y_ptr, info_ptr=info_d.data_ptr(), asynchronous=True,
+                             order_by_class=bool(args.order_by_class))
 
         def step():
             launch()
@@ -561,7 +567,8 @@ def main():
         e2e = []
         for _ in range(3):
             t_ = time.perf_counter()
-            eng.solve(syn["xref"], syn["fsteps"], mpcq.MODE_UPDATE, want_x=False)
+            eng.solve(syn["xref"], syn["fsteps"], mpcq.MODE_UPDATE, want_x=False,
+                      order_by_class=bool(args.order_by_class))
             e2e.append(time.perf_counter() - t_)
         r["e2e_ms"] = float(np.median(e2e)) * 1e3
         eng.close()
@@ -651,7 +658,10 @@ def main():
                        "instances_total": total,
                        "horizon": N, "gaits": list(cfg["gaits"]), "headline_mode": args.headline,
                        "solver": MODE_DESC[args.headline].format(ival=ival),
-                       "parallelism": f"shard{world}" + ("+gather" if args.gather else "")},
+                       "parallelism": f"shard{world}" + ("+gather" if args.gather else ""),
+                       "dispatch": ("by gait class: the mean iteration count of each instance's class over the "
+                                    "engine's earlier launches, most expensive first (MPCQ_FLAG_ORDER_BY_CLASS, in "
+                                    "the timed region)" if args.order_by_class else "index order")},
             "roofline": roof,
             "roofline_hbm": roof_hbm,
             "build": {"engine_src_sha": src_sha, "pmc_tag": pmc.get("tag"), "pmc_stale": pmc.get("stale")},

@@ -63,6 +63,13 @@ extern "C" {
 /* flags */
 #define MPCQ_FLAG_DEVICE_PTRS 1u  /* every array argument is a device pointer on ctx's device */
 #define MPCQ_FLAG_ASYNC 2u        /* do not synchronise the stream before returning (device ptrs only) */
+/* mpcq_solve_batch only: dispatch the instances in the order of the mean iteration count
+ * their gait class (the set of contact masks of their fsteps phases) has shown in this
+ * context's earlier launches with this flag, the most expensive first (index order inside
+ * a class and before any launch); the launch then adds its own counts.  Scheduling only:
+ * every result is bit-identical with and without it.  No reference counterpart (the
+ * reference solves one QP per tick). */
+#define MPCQ_FLAG_ORDER_BY_CLASS 4u
 
 /* formulation mode (MPC.py:491-494) */
 #define MPCQ_MODE_UPDATE 0  /* k > 0: update_ML/update_NK with fsteps footholds */

@@ -27,6 +27,13 @@ struct mpcq_ctx {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool have_form = false, have_solve = false;
   uint64_t* stamps = nullptr;
+  // MPCQ_FLAG_ORDER_BY_CLASS: the class table (sum of iterations, count per slot) and the
+  // per-instance scratch (class slot, dispatch order, iteration counts when the caller
+  // passes none)
+  uint64_t* cls_sum = nullptr;
+  uint32_t* cls_cnt = nullptr;
+  int32_t* ord_buf = nullptr;
+  int64_t ord_cap = 0;
 };
 
 namespace {
@@ -129,6 +136,34 @@ int ensure_work(mpcq_ctx* c, int64_t B, double** out) {
     c->work_bytes = bytes;
   }
   *out = (double*)c->work;
+  return MPCQ_OK;
+}
+
+// MPCQ_FLAG_ORDER_BY_CLASS scratch: the class table (zeroed once, kept for the context's
+// life) and 3 B int32 (class slots, order, iteration counts)
+int ensure_order(mpcq_ctx* c, int64_t B) {
+  const int slots = mpcq::class_table_slots();
+  if (!c->cls_sum) {
+    void* tab = nullptr;
+    const size_t tb = (size_t)slots * (8 + 4);
+    if (hipMalloc(&tab, tb) != hipSuccess) return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) for the class table failed", tb);
+    c->cls_sum = (uint64_t*)tab;
+    c->cls_cnt = (uint32_t*)((char*)tab + (size_t)slots * 8);
+    HIP_TRY(hipMemsetAsync(tab, 0, tb, c->stream));
+  }
+  if (B > c->ord_cap) {
+    if (c->ord_buf) {
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      HIP_TRY(hipFree(c->ord_buf));
+    }
+    c->ord_buf = nullptr;
+    c->ord_cap = 0;
+    if (hipMalloc(&c->ord_buf, (size_t)B * 12) != hipSuccess) {
+      c->ord_buf = nullptr;
+      return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) for the dispatch order failed", (size_t)B * 12);
+    }
+    c->ord_cap = B;
+  }
   return MPCQ_OK;
 }
 
@@ -294,6 +329,8 @@ int mpcq_destroy(mpcq_ctx* c) {
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   if (c->arena) (void)hipFree(c->arena);
   if (c->work) (void)hipFree(c->work);
+  if (c->cls_sum) (void)hipFree(c->cls_sum);
+  if (c->ord_buf) (void)hipFree(c->ord_buf);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -409,9 +446,22 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
   a.stamps = c->stamps;
   rc = ensure_work(c, B, &a.work);
   if (rc) return rc;
+  const bool by_class = fused && (flags & MPCQ_FLAG_ORDER_BY_CLASS);
+  int32_t *cls = nullptr, *its = a.iters;
+  if (by_class) {
+    if (B > INT32_MAX) return fail(MPCQ_E_INVALID, "MPCQ_FLAG_ORDER_BY_CLASS: batch > INT32_MAX");
+    rc = ensure_order(c, B);
+    if (rc) return rc;
+    cls = c->ord_buf;
+    int32_t* order = c->ord_buf + B;
+    if (!its) its = a.iters = c->ord_buf + 2 * B;  // (the engine writes them; the caller asked for none)
+    HIP_TRY(mpcq::launch_class_order(a.fsteps, B, cls, c->cls_sum, c->cls_cnt, order, c->stream));
+    a.order = order;
+  }
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   HIP_TRY(mpcq::launch_solve(N, fused, c->p, a, c->stream));
   HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+  if (by_class) HIP_TRY(mpcq::launch_class_learn(cls, its, B, c->cls_sum, c->cls_cnt, c->stream));
   c->have_solve = true;
   if (!dev) return unstage(c, xs, NX);
   if (!(flags & MPCQ_FLAG_ASYNC)) HIP_TRY(hipStreamSynchronize(c->stream));

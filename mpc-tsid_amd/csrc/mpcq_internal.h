@@ -108,6 +108,17 @@ hipError_t launch_retrieve(int N, const SessionArgs& a, hipStream_t s);
 // this tick's iteration counts, longest first (buckets of 16 iterations).
 hipError_t launch_order(const int32_t* iters, int64_t batch, int32_t* order, hipStream_t s);
 
+// Dispatch order of a batch solve by gait class (mpcq_order.hip, MPCQ_FLAG_ORDER_BY_CLASS):
+// cls[B] = each instance's class slot, order[B] = the instances by the expected cost their
+// class has shown on this context (sum / cnt: class_table_slots() entries), the most
+// expensive first, index order inside a cost bucket; launch_class_learn adds a launch's
+// iteration counts to the table.
+int class_table_slots();
+hipError_t launch_class_order(const double* fsteps, int64_t batch, int32_t* cls, const uint64_t* sum,
+                              const uint32_t* cnt, int32_t* order, hipStream_t s);
+hipError_t launch_class_learn(const int32_t* cls, const int32_t* iters, int64_t batch, uint64_t* sum,
+                              uint32_t* cnt, hipStream_t s);
+
 // Launchers (mpcq_engine.hip).  Return hipError_t.
 hipError_t launch_formulate(int N, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);
 hipError_t launch_solve(int N, bool fused, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);

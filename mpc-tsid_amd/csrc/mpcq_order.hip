@@ -1,0 +1,160 @@
+// mpcq_order.hip — dispatch order of a batch solve by gait class (MPCQ_FLAG_ORDER_BY_CLASS).
+//
+// The hardware hands out an engine launch's workgroups in index order, so a long solve
+// that lands in a late dispatch round ends the launch late.  A cold batch
+// has no previous tick to rank it by (the session path orders by the last tick's counts,
+// mpcq_session.hip order_kernel), and no sampled input predicts a trot QP's iteration count
+// (tools/iter_predictors.py) -- but the gait does, across gaits: on a C5 shard (trot / bound
+// / pace) trot solves take 886 iterations on average and up to 3100, bound and pace ~600
+// and up to ~1000 (Spearman -0.63, profiles/r06_iter_predictors.txt).  So:
+//   class_kernel      : per instance, its gait class: the set of contact masks its fsteps
+//                       phases use (MPC.py:635-652's contact rule), a 16-bit bitmap, folded
+//                       into one of kSlots slots of the context's class table;
+//   class_order_kernel: one workgroup: each instance's expected cost = the mean iteration
+//                       count its class slot has seen in earlier launches on this context
+//                       (the mean over every seen slot for a new class, 0 before any
+//                       launch), in buckets of 16 iterations; a stable counting sort, the
+//                       most expensive bucket first, index order inside a bucket (a batch of
+//                       one class keeps the identity order);
+//   class_learn_kernel: after the engine, each instance's iteration count into its slot.
+// Every instance's result is independent of the workgroup that solves it, so the order
+// changes no result bit (tests/test_gpu_order.py).
+#include <stdint.h>
+
+#include "mpcq_internal.h"
+
+namespace mpcq {
+namespace {
+
+constexpr int kSlots = 251;     // class table slots (a prime: the bitmap modulo it)
+constexpr int kBuckets = 256;   // expected-cost buckets of 16 iterations
+constexpr int kWaves = 16;      // the order kernel's workgroup: 1024 threads
+
+__device__ __forceinline__ int class_slot(const double* __restrict__ fs) {
+  unsigned key = 0;
+  for (int j = 0; j < 20; ++j) {
+    const double d = fs[13 * j];
+    if (d == 0.0) return (int)(key % kSlots);
+    unsigned msk = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const double x = fs[13 * j + 1 + 3 * q];
+      msk |= (!(isnan(x) || x == 0.0) ? 1u : 0u) << q;
+    }
+    key |= 1u << msk;
+  }
+  return 0;  // no terminating row: the engine reports BAD_GAIT, any slot will do
+}
+
+__global__ __launch_bounds__(256) void class_kernel(const double* __restrict__ fsteps, int64_t B,
+                                                    int32_t* __restrict__ cls) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) cls[i] = class_slot(fsteps + i * 260);
+}
+
+__global__ __launch_bounds__(1024) void class_order_kernel(const int32_t* __restrict__ cls, int64_t B,
+                                                           const unsigned long long* __restrict__ sum,
+                                                           const unsigned* __restrict__ cnt,
+                                                           int32_t* __restrict__ order) {
+  __shared__ int cost[kSlots];          // bucket of each slot
+  __shared__ int base[kBuckets];        // next free position of each bucket
+  __shared__ int wcnt[kWaves][kBuckets];
+  __shared__ unsigned long long mean_all;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  if (t == 0) {
+    unsigned long long s = 0, n = 0;
+    for (int q = 0; q < kSlots; ++q) { s += sum[q]; n += cnt[q]; }
+    mean_all = n ? s / n : 0;
+  }
+  if (t < kBuckets) base[t] = 0;
+  __syncthreads();
+  if (t < kSlots) {
+    const unsigned long long e = cnt[t] ? sum[t] / cnt[t] : mean_all;
+    const unsigned long long q = e >> 4;
+    cost[t] = q < kBuckets - 1 ? (int)q : kBuckets - 1;
+  }
+  __syncthreads();
+  for (int64_t i = t; i < B; i += blockDim.x) atomicAdd(&base[cost[cls[i]]], 1);
+  __syncthreads();
+  if (t == 0) {  // exclusive offsets, the most expensive bucket first
+    int acc = 0;
+    for (int q = kBuckets - 1; q >= 0; --q) {
+      const int h = base[q];
+      base[q] = acc;
+      acc += h;
+    }
+  }
+  __syncthreads();
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int64_t c0 = 0; c0 < B; c0 += blockDim.x) {
+    for (int e = t; e < kWaves * kBuckets; e += blockDim.x) (&wcnt[0][0])[e] = 0;
+    __syncthreads();
+    const int64_t i = c0 + t;
+    const int q = i < B ? cost[cls[i]] : -1;
+    // rank among the earlier lanes of this wave with the same bucket; per-bucket counts
+    int rank = 0;
+    bool done = q < 0;
+    for (;;) {
+      const unsigned long long pend = __ballot(!done);
+      if (!pend) break;
+      const int leader = __ffsll((long long)pend) - 1;
+      const int ql = __shfl(q, leader);
+      const unsigned long long m = __ballot(!done && q == ql);
+      if (!done && q == ql) {
+        rank = __popcll(m & below);
+        done = true;
+      }
+      if (lane == leader) wcnt[w][ql] = __popcll(m);
+    }
+    __syncthreads();
+    if (t < kBuckets) {  // waves in order: each wave's start inside the bucket
+      int run = base[t];
+#pragma unroll
+      for (int v = 0; v < kWaves; ++v) {
+        const int h = wcnt[v][t];
+        wcnt[v][t] = run;
+        run += h;
+      }
+      base[t] = run;
+    }
+    __syncthreads();
+    if (q >= 0) order[wcnt[w][q] + rank] = (int32_t)i;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void class_learn_kernel(const int32_t* __restrict__ cls,
+                                                          const int32_t* __restrict__ iters, int64_t B,
+                                                          unsigned long long* __restrict__ sum,
+                                                          unsigned* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const int32_t it = iters[i];
+  if (it <= 0) return;
+  atomicAdd(&sum[cls[i]], (unsigned long long)it);
+  atomicAdd(&cnt[cls[i]], 1u);
+}
+
+}  // namespace
+
+int class_table_slots() { return kSlots; }
+
+hipError_t launch_class_order(const double* fsteps, int64_t B, int32_t* cls, const uint64_t* sum,
+                              const uint32_t* cnt, int32_t* order, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (B > INT32_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(class_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, fsteps, B, cls);
+  hipLaunchKernelGGL(class_order_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)cls, B,
+                     (const unsigned long long*)sum, (const unsigned*)cnt, order);
+  return hipGetLastError();
+}
+
+hipError_t launch_class_learn(const int32_t* cls, const int32_t* iters, int64_t B, uint64_t* sum, uint32_t* cnt,
+                              hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(class_learn_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, cls, iters, B,
+                     (unsigned long long*)sum, (unsigned*)cnt);
+  return hipGetLastError();
+}
+
+}  // namespace mpcq

@@ -10,7 +10,7 @@ Public surface:
   synth             seeded synthetic inputs shaped like FootstepPlanner's
 """
 from . import synth  # noqa: F401
-from ._lib import (FLAG_ASYNC, FLAG_DEVICE_PTRS, MODE_SETUP, MODE_UPDATE,  # noqa: F401
+from ._lib import (FLAG_ASYNC, FLAG_DEVICE_PTRS, FLAG_ORDER_BY_CLASS, MODE_SETUP, MODE_UPDATE,  # noqa: F401
                    PLAN_FOOTSTEPS, PLAN_REFSTATES, PLAN_ROLL, PLAN_TICK, PlannerParams,
                    default_planner_params, STATUS_BAD_GAIT, SV_COST, SV_F0, SV_FSTEPS, SV_GAIT,
                    SV_H_ROT, SV_ITERS, SV_ORDER, SV_L_FEET, SV_Q_W, SV_RHO, SV_ROT_FLAG, SV_STATE, SV_STATUS, SV_X,

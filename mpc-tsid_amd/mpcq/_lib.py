@@ -51,6 +51,7 @@ STATUS_FACTOR_FAILED = -12
 STATUS_BAD_BOUNDS = -13
 FLAG_DEVICE_PTRS = 1
 FLAG_ASYNC = 2
+FLAG_ORDER_BY_CLASS = 4  # mpcq_solve_batch: dispatch by the learned cost of each gait class
 MODE_UPDATE = 0
 MODE_SETUP = 1
 PLAN_ROLL, PLAN_FOOTSTEPS, PLAN_REFSTATES = 1, 2, 4

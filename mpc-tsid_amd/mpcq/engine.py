@@ -135,9 +135,11 @@ class Engine:
                     polish_rounds=info[:, 2], admm_status=info[:, 3])
 
     def solve(self, xref, fsteps, mode: int = L.MODE_UPDATE, warm_x=None, warm_y=None, rho=None,
-              want_x: bool = True, want_y: bool = False):
+              want_x: bool = True, want_y: bool = False, order_by_class: bool = False):
         """Fused formulation + solve (mpcq_solve_batch): MPC.run's QP for a batch, with
-        the osqp workspace of the previous tick (warm_x, warm_y, rho) when given."""
+        the osqp workspace of the previous tick (warm_x, warm_y, rho) when given.
+        order_by_class: MPCQ_FLAG_ORDER_BY_CLASS (dispatch by the mean iteration count each
+        gait class has shown on this engine; results unchanged)."""
         xref, fsteps, B = self._batch_inputs(xref, fsteps)
         wx = None if warm_x is None else _f64(warm_x).reshape(B, self.n)
         wy = None if warm_y is None else _f64(warm_y).reshape(B, self.m)
@@ -150,7 +152,8 @@ class Engine:
         it = np.empty(B, np.int32)
         info = np.empty((B, 4), np.int32)
         self._call("mpcq_solve_batch", self._h, B, _p(xref), _p(fsteps), mode, _p(wx), _p(wy), _p(rin), _p(f0),
-                                         _p(x), _p(y), _p(rout), _p(st), _p(it), _p(info), 0)
+                                         _p(x), _p(y), _p(rout), _p(st), _p(it), _p(info),
+                   L.FLAG_ORDER_BY_CLASS if order_by_class else 0)
         return dict(f0=f0, x=x, y=y, rho=rout, status=st, iters=it, rho_updates=info[:, 0], polish=info[:, 1],
                     polish_rounds=info[:, 2], admm_status=info[:, 3])
 
@@ -203,8 +206,9 @@ class Engine:
     def solve_device(self, batch: int, xref_ptr: int, fsteps_ptr: int, f0_ptr: int, status_ptr: int,
                      iters_ptr: int = 0, x_ptr: int = 0, y_ptr: int = 0, mode: int = L.MODE_UPDATE,
                      warm_x_ptr: int = 0, warm_y_ptr: int = 0, info_ptr: int = 0,
-                     asynchronous: bool = False):
-        flags = L.FLAG_DEVICE_PTRS | (L.FLAG_ASYNC if asynchronous else 0)
+                     asynchronous: bool = False, order_by_class: bool = False):
+        flags = (L.FLAG_DEVICE_PTRS | (L.FLAG_ASYNC if asynchronous else 0)
+                 | (L.FLAG_ORDER_BY_CLASS if order_by_class else 0))
         v = lambda q: C.c_void_p(q) if q else None  # noqa: E731
         self._call("mpcq_solve_batch", self._h, int(batch), v(xref_ptr), v(fsteps_ptr), mode, v(warm_x_ptr),
                                          v(warm_y_ptr), None, v(f0_ptr), v(x_ptr), v(y_ptr), None, v(status_ptr),

@@ -41,6 +41,6 @@ printf '#include "mpcq_internal.h"\n#undef MPCQ_HORIZONS\n#define MPCQ_HORIZONS(
 /opt/rocm/bin/hipcc $F "$@" -I$R/include -c -o $OUT/$NAME/api.o $C/mpcq_api.cpp
 # the variant's own build stamp
 /opt/rocm/bin/hipcc $F -DMPCQ_SRC_SHA="\"$VSHA\"" -DMPCQ_ARCH='"gfx950"' -c -o $OUT/$NAME/build.o $C/mpcq_build.cpp
-/opt/rocm/bin/hipcc $F -shared -o $OUT/libmpcq_$NAME.so $OBJS $C/build/mpcq_planner.o $C/build/mpcq_session.o \
+/opt/rocm/bin/hipcc $F -shared -o $OUT/libmpcq_$NAME.so $OBJS $C/build/mpcq_planner.o $C/build/mpcq_session.o $C/build/mpcq_order.o \
   $OUT/$NAME/api.o $OUT/$NAME/build.o $OUT/$NAME/dispatch.o
 echo "built $OUT/libmpcq_$NAME.so"

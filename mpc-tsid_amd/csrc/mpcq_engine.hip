@@ -97,9 +97,9 @@ __host__ __device__ constexpr int LN(int psi) { return 4 * (psi / 3) + psi % 3; 
 // per-step pointer arithmetic.  SIG: G/H, S^-1 and the right-hand sides
 // (stages 0..N-1); SIGX: the state vectors xs[q] = X_q, q = 0..N.
 template <int N>
-__device__ __forceinline__ int SIG(int k) { return k <= N / 2 ? k : N + N / 2 - k; }
+__host__ __device__ constexpr int SIG(int k) { return k <= N / 2 ? k : N + N / 2 - k; }
 template <int N>
-__device__ __forceinline__ int SIGX(int q) { return q <= N / 2 ? q : N + N / 2 + 1 - q; }
+__host__ __device__ constexpr int SIGX(int q) { return q <= N / 2 ? q : N + N / 2 + 1 - q; }
 
 // Stage rows of the layout: a wave64 holds four 16-lane rows, so the workgroup
 // has N rounded up to a multiple of 4 rows.  The rows past N ("phantom" rows)
@@ -646,8 +646,57 @@ constexpr bool kBig = N > 32 || kOcc<N> > 2;
 // stamps); beyond 49 stages the scaled constraint values (126 N - 18 doubles) leave
 // LDS instead (N = 64: 197 KB with them, 133 KB without); the engine reads them
 // through the same accessors, the stage-parallel phases from L2.
+// The nested-dissection state solve (round 6, nd_layout in mpcq_internal.h: N = 32).  The
+// state system (block tridiagonal, 12 x 12 blocks) is split at the separator stage s = N/2
+// into A = stages 0..s-1 and B = s+1..N-1; each half is factored two-ended on its own, and
+// the ADMM loop sweeps A on wave 0 and B on wave 1 at the same time (half the depth of the
+// whole-horizon sweep), then solves for the separator's states and corrects both halves by
+// the stored spikes W_k = K_A^{-1}[k, s-1] L_s' (k in A) / K_B^{-1}[k, s+1] L_{s+1} (k in B):
+//   z = K_A^{-1} b_A, K_B^{-1} b_B      x_s = Sigma^{-1} b_s + P z_{s-1} + Q z_{s+1}
+//   x_k = z_k - W_k x_s                 Sigma = D_s - L_s W_{s-1} - L_{s+1}' W_{s+1}
+//   P = -Sigma^{-1} L_s, Q = -Sigma^{-1} L_{s+1}'
+// The spikes (N x 144 doubles) take the LDS the scaled constraint values leave (they move
+// to the workspace, kAbG) with F W at the 72-double stride.
 template <int N>
-constexpr bool kAbG = N > 49 || kOcc<N> > 2;
+constexpr bool kND = nd_layout(N);
+template <int N>
+constexpr bool kAbG = N > 49 || kOcc<N> > 2 || kND<N>;
+// (kND) the halves: A = stages 0..NDS-1, the separator NDS = N/2, B = NDS+1..N-1 (NDB stages).
+// Both halves are swept as NDS-stage systems by one code path: B's sweep carries a phantom
+// stage after its last (local stage NDB: zero right-hand side, zero coupling, zero inverse
+// slot), which it steps through in parallel with A's real one and which leaves B's solution
+// unchanged (its bottom chain starts at the phantom with v = 0).
+template <int N> constexpr int NDS = N / 2;
+template <int N> constexpr int NDB = N - 1 - N / 2;  // B's real stages (A's: NDS)
+// Sweep slots of stage k's right-hand side / w (bo, na, yv) and of its states X_{k+1} (xs).
+// Whole-horizon sweep: SIG<N>(k) / SIGX<N>(k+1).  kND: each half in its own step-ordered
+// slots (SIG / SIGX of an NDS-stage system), A's first, then B's (B's phantom at
+// NDS + SIG<NDS>(NDB)), the separator's last (right-hand side slot N, states slot N+1; B's
+// slots start at NDS so that its local X_0 -- the separator, which B's sweep never writes --
+// would be A's slot NDS).
+template <int N>
+__device__ __forceinline__ int RSL(int k) {
+  if constexpr (kND<N>) {
+    constexpr int S = NDS<N>;
+    return k < S ? SIG<S>(k) : (k == S ? N : S + SIG<S>(k - S - 1));
+  } else {
+    return SIG<N>(k);
+  }
+}
+template <int N>
+__device__ __forceinline__ int XSL(int k) {
+  if constexpr (kND<N>) {
+    constexpr int S = NDS<N>;
+    return k < S ? SIGX<S>(k + 1) : (k == S ? N + 1 : S + SIGX<S>(k - S));
+  } else {
+    return SIGX<N>(k + 1);
+  }
+}
+// (kND) GH / Sm offset of half B's slots: after A's (SLOT<NDS>'s bottom shift included);
+// B's phantom's slot (its zero H coupling in GH, its zero inverse in Sm) and right-hand side slot
+template <int N> constexpr int kGhB = GS * NDS<N> + 2;
+template <int N> constexpr int kPhSlot = kGhB<N> + SLOT<NDS<N>>(SIG<NDS<N>>(NDB<N>));
+template <int N> constexpr int kPhRhs = NDS<N> + SIG<NDS<N>>(NDB<N>);
 // Beyond 48 stages (13-16 waves: 128 VGPRs) the F_k row is read from the workspace in
 // the loop and the z update's constants are batch-loaded from private memory instead
 // of being held; from 33 to 48 stages (168 VGPRs) holding them is faster.  Measured at
@@ -683,7 +732,7 @@ template <int N> constexpr bool kLagOut = N <= 48;
 // Up to 32 stages, where the LDS has the 24 N doubles (N = 16: 80,048 B, still two
 // instances per CU).
 template <int N, bool KI = false>
-constexpr int kFWS = (!kBig<N> && !KI) ? 96 : 72;  // (kKI: the LDS goes to Z's columns)
+constexpr int kFWS = (!kBig<N> && !KI && !kND<N>) ? 96 : 72;  // (kKI: the LDS goes to Z's columns; kND: to the spikes)
 // Up to 16 stages the ADMM loop's exit status goes through LDS (Smem::flag[4]) instead of
 // a register carried across the loop: the N = 16 kernel then spills 27 instead of 43
 // VGPRs (scratch 256 -> 224 B per lane) and its C2 HBM traffic falls 127 -> 88 MB per
@@ -760,9 +809,20 @@ template <int N>
 struct Work {  // offsets (doubles) inside one instance's workspace
   // SM starts two slots in (a pad kept from round 2; the sweep no longer reads it)
   // FR: each lane's row of F_k (12 doubles, lane-interleaved: entry i of thread t at 16 kRows i + t)
-  static constexpr int SM = 2 * GS, FW = SM + N * GS + 2, QL = FW + 72 * N, ZERO = QL + 36 * N, AB = ZERO + 72,
+  // (kND: only the zero block and the scaled constraint values)
+  static constexpr int SM = 2 * GS, FW = SM + N * GS + 2, QL = FW + 72 * N, ZERO = kND<N> ? 0 : QL + 36 * N, AB = ZERO + 72,
                        FR = AB + (kAbG<N> ? ((126 * N - 18 + 1) & ~1) : 0), SIZE = FR + (N > 48 ? 12 * 16 * kRows<N> : 0);
 };
+
+// (kND) the spikes W_k (stage k's 12 x 12 block, row-major; the separator's slot unused) and
+// Sigma^{-1}, P, Q of the separator (row-major)
+template <int N>
+struct NdSmem {
+  alignas(16) double Wsp[N][GS];
+  alignas(16) double Sep[3][GS];
+  double Part[3][12];  // the separator's three terms of an iteration (ph_sweep_nd)
+};
+struct NoNdSmem {};
 
 template <int N, bool KI = false>
 struct Smem {
@@ -773,28 +833,30 @@ struct Smem {
   // dynamics-row rho of stage k [108,120); during scaling the row factors; in
   // the prologue xref / fsteps / the gait walk.
   alignas(16) double GH[N][GS];
-  double GHpad[2];  // the bottom slots' shift (SLOT)
+  double GHpad[kND<N> ? 4 : 2];  // the bottom slots' shift (SLOT; kND: both halves')
   // (N > 32: these three live in the global workspace, Work<N>)
   alignas(16) double Sm[kBig<N> ? 1 : N][GS];  // S_k^{-1} / U_k^{-1} of stage k at SLOT(SIG(k)), row-major (row stride RS)
-  double Smpad[2];
+  double Smpad[kND<N> ? 4 : 2];
   // F_k W_k (12x6, row psi at [6 psi]); W_k = B_k' R on rows 6..11: here beyond 32 stages
   // (stage stride 72), FWs at the end up to 32 stages (stride kFWS = 96)
-  alignas(16) double FWb[kBig<N> ? N : 1][(kBig<N> || !KI) ? 72 : 2];  // (kKI: no room for the placeholder)
+  alignas(16) double FWb[kBig<N> ? N : 1][(kBig<N> || (!KI && !kND<N>)) ? 72 : 2];  // (kKI / kND: no room for the placeholder)
   double QL[kBig<N> ? 1 : N][36];   // B_k F_k W_k = R^{-1} W_k' F_k W_k (6x6)
   union {
     struct {
       // sweep right-hand side of stage k's states = bo[k] + na[k]: bo from stage k
       // itself, na from stage k+1's dynamics rows (Hd (w - beta) + H6 w, summed by
       // ph_rhs); nb is scratch of the checks
-      double bo[N][12];
-      double na[N][12];
+      double bo[N + (kND<N> ? 1 : 0)][12];  // (kND: slot N the separator's, RSL)
+      double na[N + (kND<N> ? 1 : 0)][12];
       double nb[N][12];
       double yv[N][12];      // w = S^{-1} y of the inward sweep (states / duals during the checks)
-      double xs[N + 1][12];  // X_k (xs[k+1] = X_{k+1}, stage k's states)
+      double xs[N + 1 + (kND<N> ? 1 : 0)][12];  // X_k (xs[k+1] = X_{k+1}, stage k's states; kND: sweep slots, XSL)
     } it;
     struct {
       alignas(16) double St[144];  // sweep hand-offs of the factorisation (16-B aligned: the
       alignas(16) double Sb[144];  // couplings read them as column pairs)
+      alignas(16) double St2[kND<N> ? 144 : 2];  // (kND) half B's two chains
+      alignas(16) double Sb2[kND<N> ? 144 : 2];
     } fa;
   } u;
   // per-wave partial reductions (32 per wave); during the sweeps the sink of lanes
@@ -814,6 +876,8 @@ struct Smem {
   // (kKI) Z's LDS part, column-major (column c - SP0 at KVS (c - SP0)); during the
   // formation the staging of each pass.  The loop's partial products P[wave][row] sit in GH.
   alignas(16) double KV[KI ? KinvLay<N>::SPC * KinvLay<N>::KVS : 1];
+  // (kND) the spikes and the separator's matrices (no room taken at the other horizons)
+  [[no_unique_address]] std::conditional_t<kND<N>, NdSmem<N>, NoNdSmem> nd;
 };
 
 // prologue aliases inside GH
@@ -885,6 +949,9 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
     zQL = Work<N>::ZERO - Work<N>::QL;
     if (SOLVE && t < 72) wk[Work<N>::ZERO + t] = 0.0;
   } else {
+    if constexpr (ABG) {  // (kND) the zero block the masked coefficient reads of Ab point at
+      if (SOLVE && t < 72) a.work[b * Work<N>::SIZE + Work<N>::ZERO + t] = 0.0;
+    }
     SmW = (wdd*)&sh.Sm[0][0];
     FWW = (wdd*)&sh.FWs[0][0];
     QLW = (wdd*)&sh.QL[0][0];
@@ -1266,6 +1333,216 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
       }
     };
 
+      // NS: stages of the system swept (N, or a half of it under kND); RB: its right-hand
+      // side (RB[q] + RB[q + RO]), YVB: its y / w slots, XSB: its states, GHB / SMB: its G / H
+      // / M^{-1} and S^{-1} slots (ST: the stamp bucket of the wait for the right-hand sides,
+      // diagnostic builds).  ND (kND, a half on wave 0 or 1): the caller has passed the barrier
+      // that publishes the right-hand sides and runs this on the half's wave only.
+      auto ph_sweep_lag = [&](auto ns_tag, auto st_tag, auto nd_tag, lds_cd* const RB, int RO, double* const YVB,
+                              double* const XSB, lds_cd* const GHB, lds_cd* const SMB) __attribute__((always_inline)) {
+          constexpr int NS = decltype(ns_tag)::value, MID = NS / 2, BOT = NS - 1 - MID;
+          [[maybe_unused]] constexpr int ST = decltype(st_tag)::value;
+          constexpr bool ND = decltype(nd_tag)::value;
+          // P5-P7: the state solve on wave 0 alone (no block barrier inside), up to 32
+          // stages (beyond: ph_sweep_split).
+          // Inward step j = 1..MID: top kk(j) = j, bottom kk(j) = N-1-j.  Half 0 (rows
+          // 0 top / 1 bottom) runs the recurrence y_kk = b_kk - G_kk y_kk(j-1) (G_kk of
+          // the top in GH[kk], H_kk of the bottom in GH[kk+1], stored negated), one
+          // full 12-term row per lane.  Half 1 (rows 2 / 3) runs the same instruction
+          // stream on S^{-1} rows two stages behind: w_kk(j-2) = S^{-1} y_kk(j-2), its y
+          // handed over by permlane32_swap.  Step MID+1 is the meeting stage: half 0
+          // solves x_m = M^{-1} (y_m + v_m - b_m) (top and bottom rows joined by
+          // permlane16_swap), half 1 the last top w.  Then the outward sweeps.
+          const int half = (t >> 5) & 1;
+#ifndef MPCQ_REP_SWEEP
+#define MPCQ_REP_SWEEP 1
+#endif
+#pragma nounroll
+          for (int rep_ = 0; rep_ < MPCQ_REP_SWEEP; ++rep_) {  // > 1: timing experiments only
+          double xp = 0.0;
+          // Step-ordered bases (SIG): step j's rows / right-hand sides / w / X are at
+          // base + j * stride for every lane, an immediate offset.  Half 0: G_j (top,
+          // slot j) / H_{N-1-j} (bottom, slot MID+j); half 1: S^{-1} of stage kk(j-2),
+          // top slot j-2 / bottom slot MID-1+j.  Step 1's rows are iteration-invariant:
+          // wave 0 reads them before the barrier that publishes the right-hand sides.
+          // (N > 32: S^{-1} is global, so the row pointer is a generic one)
+          using swp = lds_cd;
+          using swp2 = lds_cd2;
+          swp* const GHs = GHB;
+          // (the bottom chain's slots are past N/2: +2, SLOT)
+          swp* const Mb = half == 0 ? GHs + (GS * (cr == 0 ? 0 : MID) + (cr == 0 ? 0 : kSlotPad<NS>) + RS * rr_)
+                                    : SMB + (GS * (cr == 0 ? -2 : MID - 1) + (cr == 0 ? 0 : kSlotPad<NS>) + RS * rr_);
+          double g[12];
+          auto row12 = [&](swp* q) __attribute__((always_inline)) {  // 16-B aligned row: 6 ds_read_b128
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+              const dbl2 v = ((swp2*)q)[i];
+              g[2 * i] = v.x;
+              g[2 * i + 1] = v.y;
+            }
+          };
+          // the rows of step j (j a constant after unrolling): every lane reads a slot the
+          // factorisation wrote -- the steps a chain does not take (half 1's first step,
+          // the bottom chain's steps past its BOT stages at even N) re-read a row of the
+          // chain's own, and their products are discarded by the hand-off select / the sink
+          auto rowp = [&](int j) __attribute__((always_inline)) -> swp* {
+            if (j >= 2 && j <= BOT) return Mb + GS * j;
+            const int jj = half == 0 ? (cr == 0 ? j : (j < BOT ? j : BOT))
+                                     : (cr == 0 ? (j > 2 ? j : 2) : (j < BOT + 1 ? j : BOT + 1));
+            return Mb + GS * jj;
+          };
+          STAMP(15);  // (diagnostic builds: as in ph_sweep_split)
+          if constexpr (ND) {
+            row12(rowp(1));
+          } else {
+            if (t < 64) row12(rowp(1));
+            sync_all();
+          }
+          STAMP(ST);
+          // outward step j reads G_{MID-j+1}' (top, slot MID+1-j) / H_{MID+j-1}'
+          // (bottom, slot N-j) columns: Ob + (MID - j) GS (LDS offsets are unsigned,
+          // so the bases sit at the lowest slot a chain reaches)
+          lds_cd* const Ob = GHB + (GS * (cr == 0 ? 1 : NS - MID) + (cr == 0 ? 0 : kSlotPad<NS>) + rr_);
+          if (ND || t < 64) {
+            // the sweeps are every wave's critical path (the other waves of the
+            // instance wait at the barrier): issue them ahead of a co-resident
+            // instance's stage-parallel phases
+            __builtin_amdgcn_s_setprio(3);
+            // right-hand side of step j: top stage j (slot j), bottom stage N-1-j (slot
+            // MID+1+j, except the meeting stage MID at the bottom's last step BOT, slot
+            // MID, which the bottom re-reads in the steps it does not take); na at +12N
+            lds_cd* const Bb = RB + (12 * (cr == 0 ? 0 : MID + 1) + rr_);
+            lds_cd* const Bm = RB + (12 * MID + rr_);
+            auto rhs = [&](int j) __attribute__((always_inline)) -> lds_cd* {  // j: a constant
+              return (j >= BOT && cr != 0) ? Bm : Bb + 12 * j;
+            };
+            // w of stage kk(j-2) (half 1): top slot j-2, bottom slot MID-1+j; the other
+            // lanes store into the sink with the same stride
+            lds_d* const sink = (lds_d*)&sh.red[0] + (t & 31);
+            lds_d* const Yb = (half == 1 && s < 12) ? (lds_d*)YVB + (12 * (cr == 0 ? -2 : MID - 1) + rr_)
+                                                    : sink;
+            // right-hand sides run two steps ahead: step j sums the one of step j+1
+            // (loaded during step j-1) and loads the one of step j+2; half 1 (the w
+            // products) starts its chain from 0.  The first two (y_kk(0) and step 1's)
+            // are loaded together and waited for once: they were published by the
+            // barrier just passed, so this round trip is on the critical path.
+            const double m0 = half == 0 ? 1.0 : 0.0;
+            double s0 = rhs(0)[0], s1 = rhs(0)[RO];
+            double c0 = rhs(1)[0], c1 = rhs(1)[RO];
+            asm volatile("" : "+v"(s0), "+v"(s1), "+v"(c0), "+v"(c1));
+            double src = half == 0 ? s0 + s1 : 0.0;  // y_kk(0) (half 0)
+            double bcn = (c0 + c1) * m0;
+            double b0 = rhs(2)[0], b1 = rhs(2)[RO];
+#pragma unroll
+            for (int j = 1; j <= MID + 1; ++j) {
+              asm volatile("" : : : "memory");
+              double gc[12];
+#pragma unroll
+              for (int i = 0; i < 12; ++i) gc[i] = g[i];
+              const double bc = j <= MID ? bcn : 0.0;
+              if (j < MID) {  // prefetch the next step's rows
+                row12(rowp(j + 1));
+              } else if (j == MID) {  // the meeting step: M^{-1} rows (half 0), the S walk (half 1)
+                row12(half == 0 ? GHs + RS * rr_ : rowp(MID + 1));
+                lds_cd* qb = RB + (12 * MID + rr_);
+                b0 = qb[0]; b1 = qb[RO];
+              } else {  // the last step: the first outward step's columns
+#pragma unroll
+                for (int i = 0; i < 12; ++i) g[i] = Ob[RS * i + GS * (MID - 1)];
+              }
+              asm volatile("" : : : "memory");  // the prefetch is issued here, not sunk to its use
+              double s_in = src;
+              if (j == MID + 1) s_in = half == 0 ? row_pair_sum(src) - (b0 + b1) : src;
+              const double acc = bdot12(gc, s_in, bc);
+              // the next right-hand side is summed after the chain: its loads were
+              // issued at the end of the previous step, and summing them ahead of the
+              // chain would put their LDS latency on the critical path
+              asm volatile("" : "+v"(b0), "+v"(b1));
+              if (j < MID) bcn = (b0 + b1) * m0;
+              if (j + 2 <= MID) {
+                b0 = rhs(j + 2)[0]; b1 = rhs(j + 2)[RO];
+              }
+              if (j >= 2 && j <= MID) {  // half 1: w of stage kk(j-2)
+                Yb[12 * j] = acc;
+              } else if (j == MID + 1) {  // even N: the bottom's kk(MID-1) is the meeting stage (no w)
+                if constexpr (NS & 1) Yb[12 * j] = acc;
+                else *(cr == 0 ? Yb + 12 * j : sink) = acc;
+              }
+              if (j <= MID) {
+                // half 0 continues with y_kk(j) (the bottom chain stops after step BOT), half 1
+                // receives y_kk(j-1) from half 0
+                const bool adv = j <= BOT || cr == 0;
+                src = keep_lo_take_lo(adv ? acc : src, src);
+              } else {
+                xp = acc;
+                // (lane ids from a laundered thread index: held across the loop, the
+                // condition's operand was spilled and its reload waited for here)
+                int tl_ = t;
+                asm volatile("" : "+v"(tl_));
+                if (((tl_ >> 4) & 3) == 0 && (tl_ & 15) < 12) XSB[12 * SIGX<NS>(MID + 1) + (tl_ & 15)] = xp;
+              }
+            }
+            STAMP(6);
+          }
+          if (ND || t < 64) {
+            // Outward step j: top kk = MID-j: X_kk = w_kk - G_{kk+1}' X_{kk+1}; bottom
+            // kk = MID+j: X_kk = w_kk - H_{kk-1}' X_{kk-1} (columns from Ob - j GS).  Lane
+            // rr reads column rr (a full 12-term product per lane; half 1 repeats half 0).
+            // w of stage kk: top slot MID-j, bottom slot N-j (Wb - 12 j); X_kk = xs[kk+1]:
+            // top slot MID+1-j, bottom slot N-j (SIGX; Xb - 12 j).  The bottom row's last
+            // step (kk = N) is idle: its store goes to the sink.
+            // (bases at step MID's slot: step j at base + 12 (MID - j))
+            lds_cd* const Wb = (lds_cd*)YVB + (12 * (cr == 0 ? 0 : NS - MID) + rr_);
+            lds_d* const sinkO = (lds_d*)&sh.red[0] + (t & 31);
+            lds_d* const Xb = (half == 0 && s < 12) ? (lds_d*)XSB + (12 * (cr == 0 ? 1 : NS - MID) + rr_)
+                                                    : sinkO;
+            wave_sync();  // the w written by half 1
+            double bq = Wb[12 * (MID - 1)];
+#pragma unroll
+            for (int j = 1; j <= MID; ++j) {
+              asm volatile("" : : : "memory");
+              double gc[12];
+#pragma unroll
+              for (int i = 0; i < 12; ++i) gc[i] = g[i];
+              const double bc = bq;
+              if (j < MID) {
+#pragma unroll
+                for (int i = 0; i < 12; ++i) g[i] = Ob[RS * i + GS * (MID - j - 1)];
+                // (even N: the bottom chain has no step MID; it re-reads its last w)
+                if (j + 1 <= BOT) bq = Wb[12 * (MID - j - 1)];
+                else bq = Wb[12 * (MID - (cr == 0 ? j + 1 : BOT))];
+              }
+              asm volatile("" : : : "memory");
+              const double acc = bdot12(gc, xp, bc);  // x = w - G' x_next with -G stored
+              if (j < MID) {
+                xp = acc;
+                Xb[12 * (MID - j)] = acc;
+              } else if constexpr (NS & 1) {
+                *Xb = acc;
+              } else {  // even N: the bottom chain has no step MID
+                *(cr == 0 ? Xb : sinkO) = acc;
+              }
+            }
+            __builtin_amdgcn_s_setprio(0);
+          }
+          wave_sync();
+          }  // MPCQ_REP_SWEEP
+      };
+      // (kND) Both halves' sweeps, A on wave 0 and B on wave 1, one code path (B as an NDS-stage
+      // system with its phantom): the bases differ by a wave-uniform offset.  The caller has
+      // passed the barrier that publishes the right-hand sides.
+      auto nd_sweep_halves = [&]() __attribute__((always_inline)) {
+        if constexpr (kND<N>) {
+          constexpr int S = NDS<N>;
+          const int wq = __builtin_amdgcn_readfirstlane(t >> 6);
+          if (wq < 2) {
+            const int o12 = wq ? 12 * S : 0, og = wq ? kGhB<N> : 0;
+            ph_sweep_lag(std::integral_constant<int, S>{}, std::integral_constant<int, 3>{}, std::true_type{},
+                         (lds_cd*)&sh.u.it.bo[0][0] + o12, 12 * (N + 1), &sh.u.it.yv[0][0] + o12,
+                         &sh.u.it.xs[0][0] + o12, GHr + og, (lds_cd*)&sh.Sm[0][0] + og);
+          }
+        }
+      };
     // pr: per-own-row rho override (polish: 1/delta on active rows, 0 elsewhere);
     // nullptr in the ADMM loop, where the class rho applies
     // role: std::false_type for the stage waves; std::true_type (kKI's helper waves) runs the
@@ -1423,6 +1700,157 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
         }
         schur_cols<!kBig<N>>(Ro, G, ca, c6, std::make_integer_sequence<int, 12>{});
       };
+      if constexpr (kND<N>) {
+        // (kND) Two two-ended factorisations, one per half, their steps interleaved (step j of
+        // both; B's meeting comes one step before A's at N = 32).  Half A's rows: stages
+        // 0..S-1, its top chain from stage 0, its bottom chain from S-1 (no coupling to the
+        // separator); half B's: S+1..N-1, its top chain from S+1 (no coupling to the separator).
+        // G / H / M^{-1} / S^{-1} in the half's slots (SLOT<NS>(SIG<NS>(local stage)), B's at
+        // kGhB); the chains hand off through St / Sb (A) and St2 / Sb2 (B).
+        constexpr int S = NDS<N>, NB = NDB<N>, MID2 = S / 2;
+        static_assert(S >= 4 && NB >= 3 && NB <= S, "the halves of the nested-dissection solve");
+        const int hh = k < S ? 0 : (k > S ? 1 : 2);  // 0: A, 1: B, 2: the separator
+        const int kl = hh == 0 ? k : k - S - 1;        // stage in the half
+        const int nreal = hh == 0 ? S : NB;            // (B's local stage NB is its phantom)
+        double* const Sth = hh == 0 ? St : sh.u.fa.St2;
+        double* const Sbh = hh == 0 ? Sb : sh.u.fa.Sb2;
+        const int hb = hh == 0 ? 0 : kGhB<N>;
+        auto hslot = [&](int q) __attribute__((always_inline)) -> int { return hb + SLOT<S>(SIG<S>(q)); };
+        // couple(): C S^{-1} from the given hand-off, G / H into the given slot row
+        auto couple_nd = [&](bool upper, double (&Ro)[12], const double* Sp, double* Gd)
+            __attribute__((always_inline)) {
+          const double ca = upper ? cta : cba;
+          double c6[6];
+#pragma unroll
+          for (int j = 0; j < 6; ++j) c6[j] = upper ? ct6[j] : cb6[j];
+          wave_sync();  // this row's reads of its G / H slots are done
+          const int ar = ph < 6 ? ph : ph - 6;
+          double G[12];
+#pragma unroll
+          for (int ci = 0; ci < 12; ci += 2) {
+            const dbl2 s0 = *(lds_cd2*)(Sp + 12 * ar + ci);
+            dbl2 su[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) su[j] = *(lds_cd2*)(Sp + 12 * (6 + j) + ci);
+            double g0 = ca * s0.x, g1 = ca * s0.y;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+              g0 = fma(c6[j], su[j].x, g0);
+              g1 = fma(c6[j], su[j].y, g1);
+            }
+            G[ci] = g0;
+            G[ci + 1] = g1;
+            asm volatile("" ::: "memory");
+          }
+          if (cl) {
+#pragma unroll
+            for (int ci = 0; ci < 12; ++ci) Gd[ci] = -G[ci];  // stored negated
+          }
+          schur_cols<true>(Ro, G, ca, c6, std::make_integer_sequence<int, 12>{});
+        };
+        // B's phantom: zero coupling (its G / H slot) and zero inverse (its S^{-1} slot), once the
+        // stage-keyed factor scratch in GH (Q_k, F_k W_k, rho) has been read (Drow / Ctop / Cbot)
+        sync_all();
+        for (int e = t; e < GS; e += T) {
+          gh0[kPhSlot<N> + e] = 0.0;
+          SmW[kPhSlot<N> + e] = 0.0;
+        }
+#pragma nounroll
+        for (int j = 0; j <= MID2; ++j) {
+          launder();
+          const bool act = hh < 2;
+          const bool top = act && j < MID2 && kl == j;
+          const bool bot = act && j < MID2 && kl == S - 1 - j && kl > MID2;
+          const bool mrow = act && j == MID2 && kl == MID2;
+          if (!H && (top || bot || mrow)) {
+            const bool useT = (top && kl > 0) || mrow, useB = (bot && kl < nreal - 1) || mrow;
+            double Ro[12];
+#pragma unroll
+            for (int ci = 0; ci < 12; ++ci) Ro[ci] = Dr0[ci];
+            if (useT) couple_nd(true, Ro, Sth, gh0 + hslot(kl) + RS * ph);
+            if (useB) couple_nd(false, Ro, Sbh, gh0 + hslot(kl + 1) + RS * ph);
+            gj12<true>(Ro, ph, ok);
+            if (cl) {
+#pragma unroll
+              for (int ci = 0; ci < 12; ++ci) SmW[hslot(kl) + RS * ph + ci] = Ro[ci];
+            }
+            wave_sync();  // the previous inverse has been consumed by this row
+            if (cl) {
+              double* dst = mrow ? gh0 + hb + RS * ph : (bot ? Sbh : Sth) + 12 * ph;
+#pragma unroll
+              for (int ci = 0; ci < 12; ++ci) dst[ci] = Ro[ci];
+            }
+          }
+          sync_all();
+        }
+        // The spikes: each half solved with its coupling to the separator as the right-hand
+        // side, one column at a time through the ADMM loop's own half sweeps -- A with column
+        // cI of L_s' at stage S-1 (row ph of L_s' is stage S-1's lower coupling row, cba /
+        // cb6), B with column cI of L_{S+1} at stage S+1 (its upper coupling row, cta / ct6);
+        // W_k = the solution's block at stage k.  (u.fa's hand-offs are dead: u.it's right-hand
+        // sides, w and states take their place.)
+        {
+          const int ar = ph < 6 ? ph : ph - 6;
+#pragma nounroll
+          for (int cI = 0; cI < 12; ++cI) {
+            launder();
+            const bool lo = k == S - 1, up = k == S + 1;
+            double ca = lo ? cba : cta, cv = 0.0;
+#pragma unroll
+            for (int j = 0; j < 6; ++j)
+              if (cI == 6 + j) cv = lo ? cb6[j] : ct6[j];
+            const double rv = (lo || up) ? (cI == ar ? ca : 0.0) + cv : 0.0;
+            if (cl) {
+              sh.u.it.bo[RSL<N>(k)][ph] = rv;
+              sh.u.it.na[RSL<N>(k)][ph] = 0.0;
+              if (k == S) { sh.u.it.bo[kPhRhs<N>][ph] = 0.0; sh.u.it.na[kPhRhs<N>][ph] = 0.0; }
+            }
+            sync_all();
+            nd_sweep_halves();
+            sync_all();
+            if (cl && k != S) sh.nd.Wsp[k][RS * ph + cI] = sh.u.it.xs[XSL<N>(k)][ph];
+          }
+        }
+        sync_all();
+        // The separator: Sigma = D_S - L_S W_{S-1} - L_{S+1}' W_{S+1} (row ph: stage S's upper
+        // coupling row cta / ct6 against W_{S-1}, its lower one cba / cb6 against W_{S+1}), its
+        // inverse, P = -Sigma^{-1} L_S and Q = -Sigma^{-1} L_{S+1}' (rows of L_S / L_{S+1}' from
+        // the row's lanes by broadcast).
+        if (k == S) {
+          const int ar = ph < 6 ? ph : ph - 6;
+          double Ro[12];
+#pragma unroll
+          for (int ci = 0; ci < 12; ++ci) {
+            const double* const Wa = &sh.nd.Wsp[S - 1][0];
+            const double* const Wb = &sh.nd.Wsp[S + 1][0];
+            double ga = cta * Wa[12 * ar + ci], gb = cba * Wb[12 * ar + ci];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+              ga = fma(ct6[j], Wa[12 * (6 + j) + ci], ga);
+              gb = fma(cb6[j], Wb[12 * (6 + j) + ci], gb);
+            }
+            Ro[ci] = Dr0[ci] - ga - gb;
+          }
+          gj12<true>(Ro, ph, ok);
+          double Pr[12], Qr[12];
+#pragma unroll
+          for (int c = 0; c < 12; ++c) {
+            const double lt = (c == ar ? cta : 0.0) + (c >= 6 ? ct6[c >= 6 ? c - 6 : 0] : 0.0);
+            const double lb = (c == ar ? cba : 0.0) + (c >= 6 ? cb6[c >= 6 ? c - 6 : 0] : 0.0);
+            Pr[c] = -bdot_ln12(Ro, lt, 0.0);
+            Qr[c] = -bdot_ln12(Ro, lb, 0.0);
+          }
+          if (cl) {
+#pragma unroll
+            for (int ci = 0; ci < 12; ++ci) {
+              sh.nd.Sep[0][RS * ph + ci] = Ro[ci];
+              sh.nd.Sep[1][RS * ph + ci] = Pr[ci];
+              sh.nd.Sep[2][RS * ph + ci] = Qr[ci];
+            }
+          }
+        }
+        sync_all();
+      } else {
       // Step j < MID: top row k = j and bottom row k = N-1-j > MID in parallel; step
       // MID: the meeting row (both couplings).  M^{-1} -> GH[0].
 #pragma nounroll
@@ -1451,6 +1879,7 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
         }
         sync_all();
       }
+      }  // kND
       STAMP(14);
       // a non-positive pivot anywhere fails the whole instance (uniform result)
       if (!ok) atomicOr(&sh.flag[2], 1);
@@ -1507,7 +1936,7 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
       o.oXSp = 12 * k + ph;  // natural order (update_info)
       o.oXSp6 = 12 * k + (ph < 6 ? ph + 6 : ph);
       // the sweep's states in its slots (SIGX): own X_{k+1}, the previous stage's X_k
-      auto xsl = [](int kk) __attribute__((always_inline)) -> int { return 12 * SIGX<N>(kk + 1); };
+      auto xsl = [](int kk) __attribute__((always_inline)) -> int { return 12 * XSL<N>(kk); };
       o.rXS = xsl(k) + ph;
       o.rXSpm = hp_ ? xsl(k - 1) + ph : zXS;
       o.rXSp6m = hp_ ? xsl(k - 1) + (ph < 6 ? ph + 6 : ph) : zXS;
@@ -1520,8 +1949,8 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
         o.Wbo = &sh.u.it.bo[k][ph];
         o.Wna = &sh.u.it.na[hp_ ? k - 1 : N - 1][ph];
       } else {
-        o.Wbo = &sh.u.it.bo[SIG<N>(k)][ph];
-        o.Wna = &sh.u.it.na[SIG<N>(hp_ ? k - 1 : N - 1)][ph];
+        o.Wbo = &sh.u.it.bo[RSL<N>(k)][ph];
+        o.Wna = &sh.u.it.na[RSL<N>(hp_ ? k - 1 : N - 1)][ph];
       }
       return o;
     };
@@ -2278,6 +2707,12 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
             } else {
               *(cl ? Wna : Wdump) = na + nbx;
             }
+            if constexpr (kND<N>) {  // B's phantom reads a zero right-hand side (the checks scribble on u.it)
+              if (k == NDS<N> && cl) {
+                sh.u.it.bo[kPhRhs<N>][ph] = 0.0;
+                sh.u.it.na[kPhRhs<N>][ph] = 0.0;
+              }
+            }
           }
           // (the barrier that publishes bo / na / nb opens ph_sweep)
       };
@@ -2514,201 +2949,89 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
           wave_sync();
           }  // MPCQ_REP_SWEEP
       };
-      // NS: stages of the system swept (N, or N / 2 after the cyclic reduction); RB: its
-      // right-hand side (RB[q] + RB[q + RO]), YVB: its y / w slots, XSB: its states
-      // (ST: the stamp bucket of the wait for the right-hand sides, diagnostic builds)
-      auto ph_sweep_lag = [&](auto ns_tag, auto st_tag, lds_cd* const RB, int RO, double* const YVB,
-                              double* const XSB) __attribute__((always_inline)) {
-          constexpr int NS = decltype(ns_tag)::value, MID = NS / 2, BOT = NS - 1 - MID;
-          [[maybe_unused]] constexpr int ST = decltype(st_tag)::value;
-          // P5-P7: the state solve on wave 0 alone (no block barrier inside), up to 32
-          // stages (beyond: ph_sweep_split).
-          // Inward step j = 1..MID: top kk(j) = j, bottom kk(j) = N-1-j.  Half 0 (rows
-          // 0 top / 1 bottom) runs the recurrence y_kk = b_kk - G_kk y_kk(j-1) (G_kk of
-          // the top in GH[kk], H_kk of the bottom in GH[kk+1], stored negated), one
-          // full 12-term row per lane.  Half 1 (rows 2 / 3) runs the same instruction
-          // stream on S^{-1} rows two stages behind: w_kk(j-2) = S^{-1} y_kk(j-2), its y
-          // handed over by permlane32_swap.  Step MID+1 is the meeting stage: half 0
-          // solves x_m = M^{-1} (y_m + v_m - b_m) (top and bottom rows joined by
-          // permlane16_swap), half 1 the last top w.  Then the outward sweeps.
-          const int half = (t >> 5) & 1;
-#ifndef MPCQ_REP_SWEEP
-#define MPCQ_REP_SWEEP 1
-#endif
-#pragma nounroll
-          for (int rep_ = 0; rep_ < MPCQ_REP_SWEEP; ++rep_) {  // > 1: timing experiments only
-          double xp = 0.0;
-          // Step-ordered bases (SIG): step j's rows / right-hand sides / w / X are at
-          // base + j * stride for every lane, an immediate offset.  Half 0: G_j (top,
-          // slot j) / H_{N-1-j} (bottom, slot MID+j); half 1: S^{-1} of stage kk(j-2),
-          // top slot j-2 / bottom slot MID-1+j.  Step 1's rows are iteration-invariant:
-          // wave 0 reads them before the barrier that publishes the right-hand sides.
-          // (N > 32: S^{-1} is global, so the row pointer is a generic one)
-          using swp = lds_cd;
-          using swp2 = lds_cd2;
-          swp* const GHs = GHr;
-          // (the bottom chain's slots are past N/2: +2, SLOT)
-          swp* const Mb = half == 0 ? GHs + (GS * (cr == 0 ? 0 : MID) + (cr == 0 ? 0 : kSlotPad<NS>) + RS * rr_)
-                                    : (lds_cd*)&sh.Sm[0][0] + (GS * (cr == 0 ? -2 : MID - 1) + (cr == 0 ? 0 : kSlotPad<NS>) + RS * rr_);
-          double g[12];
-          auto row12 = [&](swp* q) __attribute__((always_inline)) {  // 16-B aligned row: 6 ds_read_b128
+      // ph_recover's iteration-invariant operands (F W and R^{-1} Q rows, friction coefficients)
+      struct RecPre {
+        double fwl[6], qll[6], cFb, cFa, cF4;
+      };
+      auto rec_pre = [&](RecPre& r) __attribute__((always_inline)) {
+        MPCQ_LANE_OFFS(kRecompLoop);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {  // 16-B aligned pairs: ds_read_b128 (twice ds_read2_b64's LDS rate)
+          using wcd2 = std::conditional_t<BIG, const dbl2, lds_cd2>;
+          const dbl2 fa = ((lds_cd2*)(FWr + oFW))[i], qa = ((wcd2*)(QLr + oQLm))[i];
+          r.fwl[2 * i] = fa.x; r.fwl[2 * i + 1] = fa.y;
+          r.qll[2 * i] = qa.x; r.qll[2 * i + 1] = qa.y;
+        }
+        r.cFb = Ab[oFb]; r.cFa = Ab[oFa]; r.cF4 = Ab[oF4];
+      };
+      // (kND) The state solve by nested dissection: the halves swept at once (A on wave 0, B on
+      // wave 1, each ph_sweep_lag's two-ended sweep on its own slots); wave 0 then forms
+      // P z_{S-1} and wave 1 Q z_{S+1} (each on its sweep lanes, lane r = component r: the half's
+      // separator-side state and the P / Q rows from LDS), the separator row's lanes Sigma^{-1}
+      // b_S meanwhile (b_S is published); one barrier; then every lane sums the separator's
+      // states x_S = Sigma^{-1} b_S + P z_{S-1} + Q z_{S+1} and corrects its own:
+      // x_k = z_k - W_k x_S.  ph_recover's barrier publishes the corrected states.  pre: the
+      // iteration-invariant operands of ph_recover, read right after the sweeps (their latency
+      // -- L2 for the constraint values -- behind the barrier and the correction).
+      auto ph_sweep_nd = [&](RecPre* pre) __attribute__((always_inline)) {
+        if constexpr (kND<N>) {
+          constexpr int S = NDS<N>;
+          sync_all();  // the right-hand sides (ph_rhs)
+          const int wq = __builtin_amdgcn_readfirstlane(t >> 6);
+          lds_d* const part = (lds_d*)&sh.nd.Part[0][0];  // [0]: P z_{S-1}, [1]: Q z_{S+1}, [2]: Sigma^{-1} b_S
+          nd_sweep_halves();
+          if (wq < 2) {  // (the sweep's own wave_sync has published its states to the wave)
+            // (lane ids from a laundered thread index: held across the loop, these addresses were
+            // spilled and each reload waited for)
+            int tl_ = t;
+            asm volatile("" : "+v"(tl_));
+            const int ri = (tl_ & 15) < 12 ? (tl_ & 15) : (tl_ & 15) - 12;
+            const double zv = sh.u.it.xs[XSL<N>(wq == 0 ? S - 1 : S + 1)][ri];
+            double pr[12];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-              const dbl2 v = ((swp2*)q)[i];
-              g[2 * i] = v.x;
-              g[2 * i + 1] = v.y;
+              const dbl2 v = ((lds_cd2*)&sh.nd.Sep[1 + wq][RS * ri])[i];
+              pr[2 * i] = v.x; pr[2 * i + 1] = v.y;
             }
-          };
-          // the rows of step j (j a constant after unrolling): every lane reads a slot the
-          // factorisation wrote -- the steps a chain does not take (half 1's first step,
-          // the bottom chain's steps past its BOT stages at even N) re-read a row of the
-          // chain's own, and their products are discarded by the hand-off select / the sink
-          auto rowp = [&](int j) __attribute__((always_inline)) -> swp* {
-            if (j >= 2 && j <= BOT) return Mb + GS * j;
-            const int jj = half == 0 ? (cr == 0 ? j : (j < BOT ? j : BOT))
-                                     : (cr == 0 ? (j > 2 ? j : 2) : (j < BOT + 1 ? j : BOT + 1));
-            return Mb + GS * jj;
-          };
-          STAMP(15);  // (diagnostic builds: as in ph_sweep_split)
-          if (t < 64) row12(rowp(1));
-          sync_all();
-          STAMP(ST);
-          // outward step j reads G_{MID-j+1}' (top, slot MID+1-j) / H_{MID+j-1}'
-          // (bottom, slot N-j) columns: Ob + (MID - j) GS (LDS offsets are unsigned,
-          // so the bases sit at the lowest slot a chain reaches)
-          lds_cd* const Ob = GHr + (GS * (cr == 0 ? 1 : NS - MID) + (cr == 0 ? 0 : kSlotPad<NS>) + rr_);
-          if (t < 64) {
-            // the sweeps are every wave's critical path (the other waves of the
-            // instance wait at the barrier): issue them ahead of a co-resident
-            // instance's stage-parallel phases
-            __builtin_amdgcn_s_setprio(3);
-            // right-hand side of step j: top stage j (slot j), bottom stage N-1-j (slot
-            // MID+1+j, except the meeting stage MID at the bottom's last step BOT, slot
-            // MID, which the bottom re-reads in the steps it does not take); na at +12N
-            lds_cd* const Bb = RB + (12 * (cr == 0 ? 0 : MID + 1) + rr_);
-            lds_cd* const Bm = RB + (12 * MID + rr_);
-            auto rhs = [&](int j) __attribute__((always_inline)) -> lds_cd* {  // j: a constant
-              return (j >= BOT && cr != 0) ? Bm : Bb + 12 * j;
-            };
-            // w of stage kk(j-2) (half 1): top slot j-2, bottom slot MID-1+j; the other
-            // lanes store into the sink with the same stride
-            lds_d* const sink = (lds_d*)&sh.red[0] + (t & 31);
-            lds_d* const Yb = (half == 1 && s < 12) ? (lds_d*)YVB + (12 * (cr == 0 ? -2 : MID - 1) + rr_)
-                                                    : sink;
-            // right-hand sides run two steps ahead: step j sums the one of step j+1
-            // (loaded during step j-1) and loads the one of step j+2; half 1 (the w
-            // products) starts its chain from 0.  The first two (y_kk(0) and step 1's)
-            // are loaded together and waited for once: they were published by the
-            // barrier just passed, so this round trip is on the critical path.
-            const double m0 = half == 0 ? 1.0 : 0.0;
-            double s0 = rhs(0)[0], s1 = rhs(0)[RO];
-            double c0 = rhs(1)[0], c1 = rhs(1)[RO];
-            asm volatile("" : "+v"(s0), "+v"(s1), "+v"(c0), "+v"(c1));
-            double src = half == 0 ? s0 + s1 : 0.0;  // y_kk(0) (half 0)
-            double bcn = (c0 + c1) * m0;
-            double b0 = rhs(2)[0], b1 = rhs(2)[RO];
+            const double pz = bdot12(pr, zv, 0.0);
+            if (((tl_ >> 4) & 3) == 0 && (tl_ & 15) < 12) part[12 * wq + ri] = pz;
+          } else if (k == S) {
+            double Si[12];
 #pragma unroll
-            for (int j = 1; j <= MID + 1; ++j) {
-              asm volatile("" : : : "memory");
-              double gc[12];
-#pragma unroll
-              for (int i = 0; i < 12; ++i) gc[i] = g[i];
-              const double bc = j <= MID ? bcn : 0.0;
-              if (j < MID) {  // prefetch the next step's rows
-                row12(rowp(j + 1));
-              } else if (j == MID) {  // the meeting step: M^{-1} rows (half 0), the S walk (half 1)
-                row12(half == 0 ? GHs + RS * rr_ : rowp(MID + 1));
-                lds_cd* qb = RB + (12 * MID + rr_);
-                b0 = qb[0]; b1 = qb[RO];
-              } else {  // the last step: the first outward step's columns
-#pragma unroll
-                for (int i = 0; i < 12; ++i) g[i] = Ob[RS * i + GS * (MID - 1)];
-              }
-              asm volatile("" : : : "memory");  // the prefetch is issued here, not sunk to its use
-              double s_in = src;
-              if (j == MID + 1) s_in = half == 0 ? row_pair_sum(src) - (b0 + b1) : src;
-              const double acc = bdot12(gc, s_in, bc);
-              // the next right-hand side is summed after the chain: its loads were
-              // issued at the end of the previous step, and summing them ahead of the
-              // chain would put their LDS latency on the critical path
-              asm volatile("" : "+v"(b0), "+v"(b1));
-              if (j < MID) bcn = (b0 + b1) * m0;
-              if (j + 2 <= MID) {
-                b0 = rhs(j + 2)[0]; b1 = rhs(j + 2)[RO];
-              }
-              if (j >= 2 && j <= MID) {  // half 1: w of stage kk(j-2)
-                Yb[12 * j] = acc;
-              } else if (j == MID + 1) {  // even N: the bottom's kk(MID-1) is the meeting stage (no w)
-                if constexpr (NS & 1) Yb[12 * j] = acc;
-                else *(cr == 0 ? Yb + 12 * j : sink) = acc;
-              }
-              if (j <= MID) {
-                // half 0 continues with y_kk(j) (the bottom chain stops after step BOT), half 1
-                // receives y_kk(j-1) from half 0
-                const bool adv = j <= BOT || cr == 0;
-                src = keep_lo_take_lo(adv ? acc : src, src);
-              } else {
-                xp = acc;
-                // (lane ids from a laundered thread index: held across the loop, the
-                // condition's operand was spilled and its reload waited for here)
-                int tl_ = t;
-                asm volatile("" : "+v"(tl_));
-                if (((tl_ >> 4) & 3) == 0 && (tl_ & 15) < 12) XSB[12 * SIGX<NS>(MID + 1) + (tl_ & 15)] = xp;
-              }
+            for (int i = 0; i < 6; ++i) {
+              const dbl2 v = ((lds_cd2*)&sh.nd.Sep[0][RS * ph])[i];
+              Si[2 * i] = v.x; Si[2 * i + 1] = v.y;
             }
-            STAMP(6);
+            const double bs = sh.u.it.bo[N - 1][ph] + sh.u.it.na[N - 1][ph];  // b_S (RSL: slot N-1)
+            const double sb = bdot_ln12(Si, bs, 0.0);
+            if (cl) part[24 + ph] = sb;
           }
-          if (t < 64) {
-            // Outward step j: top kk = MID-j: X_kk = w_kk - G_{kk+1}' X_{kk+1}; bottom
-            // kk = MID+j: X_kk = w_kk - H_{kk-1}' X_{kk-1} (columns from Ob - j GS).  Lane
-            // rr reads column rr (a full 12-term product per lane; half 1 repeats half 0).
-            // w of stage kk: top slot MID-j, bottom slot N-j (Wb - 12 j); X_kk = xs[kk+1]:
-            // top slot MID+1-j, bottom slot N-j (SIGX; Xb - 12 j).  The bottom row's last
-            // step (kk = N) is idle: its store goes to the sink.
-            // (bases at step MID's slot: step j at base + 12 (MID - j))
-            lds_cd* const Wb = (lds_cd*)YVB + (12 * (cr == 0 ? 0 : NS - MID) + rr_);
-            lds_d* const sinkO = (lds_d*)&sh.red[0] + (t & 31);
-            lds_d* const Xb = (half == 0 && s < 12) ? (lds_d*)XSB + (12 * (cr == 0 ? 1 : NS - MID) + rr_)
-                                                    : sinkO;
-            wave_sync();  // the w written by half 1
-            double bq = Wb[12 * (MID - 1)];
+          if (pre) rec_pre(*pre);
+          sync_all();  // z of both halves, the separator's three terms
+          const double xv = (part[24 + ph] + part[ph]) + part[12 + ph];
+          double Wr[12];
 #pragma unroll
-            for (int j = 1; j <= MID; ++j) {
-              asm volatile("" : : : "memory");
-              double gc[12];
-#pragma unroll
-              for (int i = 0; i < 12; ++i) gc[i] = g[i];
-              const double bc = bq;
-              if (j < MID) {
-#pragma unroll
-                for (int i = 0; i < 12; ++i) g[i] = Ob[RS * i + GS * (MID - j - 1)];
-                // (even N: the bottom chain has no step MID; it re-reads its last w)
-                if (j + 1 <= BOT) bq = Wb[12 * (MID - j - 1)];
-                else bq = Wb[12 * (MID - (cr == 0 ? j + 1 : BOT))];
-              }
-              asm volatile("" : : : "memory");
-              const double acc = bdot12(gc, xp, bc);  // x = w - G' x_next with -G stored
-              if (j < MID) {
-                xp = acc;
-                Xb[12 * (MID - j)] = acc;
-              } else if constexpr (NS & 1) {
-                *Xb = acc;
-              } else {  // even N: the bottom chain has no step MID
-                *(cr == 0 ? Xb : sinkO) = acc;
-              }
-            }
-            __builtin_amdgcn_s_setprio(0);
+          for (int i = 0; i < 6; ++i) {
+            const dbl2 v = ((lds_cd2*)&sh.nd.Wsp[k][RS * ph])[i];
+            Wr[2 * i] = v.x; Wr[2 * i + 1] = v.y;
           }
-          wave_sync();
-          }  // MPCQ_REP_SWEEP
+          const double corr = bdot_ln12(Wr, xv, 0.0);
+          double* const zk = &sh.u.it.xs[XSL<N>(k)][ph];
+          const double zv = *zk;
+          if (cl) *zk = k == S ? xv : zv - corr;
+        }
       };
       // the state sweep: the lagging form up to 32 stages, the split form beyond
+      // (kND: the nested-dissection solve)
       auto ph_sweep = [&]() __attribute__((always_inline)) {
-        if constexpr (BIG) {
+        if constexpr (kND<N>) {
+          ph_sweep_nd(nullptr);
+        } else if constexpr (BIG) {
           ph_sweep_split();
         } else {
-          ph_sweep_lag(std::integral_constant<int, N>{}, std::integral_constant<int, 3>{},
-                       (lds_cd*)&sh.u.it.bo[0][0], 12 * N, &sh.u.it.yv[0][0], &sh.u.it.xs[0][0]);
+          ph_sweep_lag(std::integral_constant<int, N>{}, std::integral_constant<int, 3>{}, std::false_type{},
+                       (lds_cd*)&sh.u.it.bo[0][0], 12 * N, &sh.u.it.yv[0][0], &sh.u.it.xs[0][0], GHr,
+                       (lds_cd*)&sh.Sm[0][0]);
         }
       };
       // (kKI) the state x_i = sum over the eight waves' partial products P[w][i] (in GH), always
@@ -2722,7 +3045,7 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
       };
       // ri0: 1/rho of the own slot-0 row (the ADMM loop's, or polish's)
       auto ph_recover = [&](const RhsOps* op, double ri0, double uf, double beta, double& sf, double& sX,
-                            double (&ax)[3])
+                            double (&ax)[3], const RecPre* pre = nullptr)
           __attribute__((always_inline)) {
           // P8: forces f_k = F_k (b_f - R B' g) = u - (F W) g, with g = Xd X_{k+1} + Hd X_k
           // on the velocity rows (the states' part of those rows)
@@ -2730,18 +3053,28 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
           MPCQ_LANE_OFFS(kRecompLoop);
           // the iteration-invariant LDS operands of P8 / P9 are read before the
           // barrier that ends the sweeps (their latency hides behind it), the
-          // sweep's states after it
-          double fwl[6], qll[6];
+          // sweep's states after it (kND: read by ph_sweep_nd, pre)
+          double fwl[6], qll[6], cFb, cFa, cF4;
+          if constexpr (kND<N>) {
+            RecPre own_;
+            if (!pre) rec_pre(own_);
+            const RecPre& q_ = pre ? *pre : own_;
 #pragma unroll
-          for (int i = 0; i < 3; ++i) {  // 16-B aligned pairs: ds_read_b128 (twice ds_read2_b64's LDS rate)
-            using wcd2 = std::conditional_t<BIG, const dbl2, lds_cd2>;
-            const dbl2 fa = ((lds_cd2*)(FWr + oFW))[i], qa = ((wcd2*)(QLr + oQLm))[i];
-            fwl[2 * i] = fa.x; fwl[2 * i + 1] = fa.y;
-            qll[2 * i] = qa.x; qll[2 * i + 1] = qa.y;
+            for (int i = 0; i < 6; ++i) { fwl[i] = q_.fwl[i]; qll[i] = q_.qll[i]; }
+            cFb = q_.cFb; cFa = q_.cFa; cF4 = q_.cF4;
+          } else {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {  // 16-B aligned pairs: ds_read_b128 (twice ds_read2_b64's LDS rate)
+              using wcd2 = std::conditional_t<BIG, const dbl2, lds_cd2>;
+              const dbl2 fa = ((lds_cd2*)(FWr + oFW))[i], qa = ((wcd2*)(QLr + oQLm))[i];
+              fwl[2 * i] = fa.x; fwl[2 * i + 1] = fa.y;
+              qll[2 * i] = qa.x; qll[2 * i + 1] = qa.y;
+            }
           }
           // (the same coefficients as ph_rhs's, from the held set when there is one)
           const double eXd = op ? op->cXd : Ab[oXd], eHd = op ? op->cHd : Ab[oHdm], eH6 = op ? op->cH6 : Ab[oH6m];
-          const double cFb = Ab[oFb], cFa = Ab[oFa], cF4 = Ab[oF4], cSw = op ? op->cf[4] : Ab[oF + 4];
+          if constexpr (!kND<N>) { cFb = Ab[oFb]; cFa = Ab[oFa]; cF4 = Ab[oF4]; }
+          const double cSw = op ? op->cf[4] : Ab[oF + 4];
           sync_all();
           STAMP(7);
           double xa, xb;
@@ -3138,7 +3471,9 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
           // register budget of the 9..16-wave workgroups -- N = 48: scratch 840 -> 712 B
           // per lane, 17.68 -> 16.75 us per iteration, profiles/r03c_iterbench.txt)
           ph_rhs(true, kBig<N> ? nullptr : &ops, kNoW, 0.0, 0.0, uf, beta);
-          ph_sweep();
+          [[maybe_unused]] RecPre pre_;
+          if constexpr (kND<N>) ph_sweep_nd(&pre_);
+          else ph_sweep();
           // DELTA (the last iteration before a check): the check's constant block is read
           // here, its memory latency behind the force recovery and the z / y / x update
           if constexpr (DELTA) ck_all(cvp);
@@ -3151,7 +3486,7 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
               zl[j] = q[ZC_LO + j]; zh[j] = q[ZC_HI + j]; zrr[j] = q[ZC_RR + j]; zri[j] = q[ZC_RI + j];
             }
           } else {
-            ph_recover(kBig<N> ? nullptr : &ops, ri[0], uf, beta, sf, sX, ax);
+            ph_recover(kBig<N> ? nullptr : &ops, ri[0], uf, beta, sf, sX, ax, kND<N> ? &pre_ : nullptr);
 #pragma unroll
             for (int j = 0; j < 3; ++j) { zl[j] = lo_of(j); zh[j] = hi_of(j); zrr[j] = rr[j]; zri[j] = ri[j]; }
           }
@@ -3479,7 +3814,7 @@ template <int N>
 hipError_t launch_t(bool fused, bool solve, const mpcq_params& p, const LaunchArgs& a,
                     hipStream_t s) {
   const dim3 grid((unsigned)a.batch), block(16 * kRows<N>), block2(16 * kRows<N> * (kKinv<N> ? 2 : 1));
-  if (kBig<N> && solve && !a.work) return hipErrorInvalidValue;  // the caller sizes it with work_doubles(N)
+  if ((kBig<N> || kND<N>) && solve && !a.work) return hipErrorInvalidValue;  // the caller sizes it with work_doubles(N)
   // polish lives in its own instantiation: the production kernel's code (and its
   // register allocation in the ADMM loop) does not carry it
   const bool pol = p.polish != 0;
@@ -3501,7 +3836,8 @@ hipError_t launch_t(bool fused, bool solve, const mpcq_params& p, const LaunchAr
 static_assert(MPCQ_ENGINE_N >= 4 && kRows<MPCQ_ENGINE_N> <= 64, "horizons 4..64 (1024 threads at most)");
 static_assert(sizeof(Smem<MPCQ_ENGINE_N>) <= 160 * 1024, "Smem<N> exceeds the CU's LDS");
 static_assert(sizeof(Smem<MPCQ_ENGINE_N, kKinv<MPCQ_ENGINE_N>>) <= 160 * 1024, "Smem<N, KI> exceeds the CU's LDS");
-static_assert(Work<MPCQ_ENGINE_N>::SIZE == (kBig<MPCQ_ENGINE_N> ? work_doubles(MPCQ_ENGINE_N) : 72 + Work<MPCQ_ENGINE_N>::ZERO),
+static_assert(Work<MPCQ_ENGINE_N>::SIZE == ((kBig<MPCQ_ENGINE_N> || kND<MPCQ_ENGINE_N>) ? work_doubles(MPCQ_ENGINE_N)
+                                                                                   : 72 + Work<MPCQ_ENGINE_N>::ZERO),
               "work_doubles(N) (mpcq_internal.h) and Work<N> disagree");
 static_assert(kRows<MPCQ_ENGINE_N> > 16 || sizeof(Smem<MPCQ_ENGINE_N>) <= 80 * 1024,
               "Smem<N> must fit twice in a CU for N <= 16");

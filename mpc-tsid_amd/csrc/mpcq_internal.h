@@ -31,7 +31,7 @@ struct LaunchArgs {
   double* rho_out;     // [B]
   int32_t* info;       // [B][4]: rho updates, polish status, polish rounds, reserved
   uint64_t* stamps;    // [B][16] diagnostic build only (MPCQ_STAMPS): cycles per phase
-  double* work;        // [B][work_doubles(N)] engine workspace (N > 32 only, else unused)
+  double* work;        // [B][work_doubles(N)] engine workspace (N > 32 and the nested-dissection horizons)
   const int32_t* order; // [B] instance solved by workgroup i (a permutation of 0..B-1), or null: i
 };
 
@@ -52,7 +52,17 @@ constexpr bool work_occ16(int N) { return N == 16 && MPCQ_OCC16 > 2; }
 #else
 constexpr bool work_occ16(int) { return false; }
 #endif
+// The nested-dissection state solve (mpcq_engine.hip kND, round 6): at these horizons the
+// scaled constraint values live in the workspace (72-double zero block + 126 N - 18, rounded
+// up to even), which frees the LDS for the separator's spikes.  -DMPCQ_NO_ND: the round-5
+// two-ended sweep at every horizon.
+#ifdef MPCQ_NO_ND
+constexpr bool nd_layout(int) { return false; }
+#else
+constexpr bool nd_layout(int N) { return N == 32; }
+#endif
 constexpr int64_t work_doubles(int N) {
+  if (nd_layout(N)) return 72 + ((126 * (int64_t)N - 18 + 1) & ~1);
   return (N > 32 || work_occ16(N)) ? 288 + (int64_t)N * (144 + 72 + 36) + 2 + 72 + ((N > 49 || work_occ16(N)) ? ((126 * N - 18 + 1) & ~1) : 0) +
                       (N > 48 ? (int64_t)12 * 16 * ((N + 3) & ~3) : 0)
                 : 0;

@@ -697,6 +697,9 @@ __device__ __forceinline__ int XSL(int k) {
 template <int N> constexpr int kGhB = GS * NDS<N> + 2;
 template <int N> constexpr int kPhSlot = kGhB<N> + SLOT<NDS<N>>(SIG<NDS<N>>(NDB<N>));
 template <int N> constexpr int kPhRhs = NDS<N> + SIG<NDS<N>>(NDB<N>);
+// (kND) stage k's spike block (k != NDS)
+template <int N>
+__device__ __forceinline__ int WSI(int k) { return k < NDS<N> ? k : k - 1; }
 // Beyond 48 stages (13-16 waves: 128 VGPRs) the F_k row is read from the workspace in
 // the loop and the z update's constants are batch-loaded from private memory instead
 // of being held; from 33 to 48 stages (168 VGPRs) holding them is faster.  Measured at
@@ -818,7 +821,7 @@ struct Work {  // offsets (doubles) inside one instance's workspace
 // Sigma^{-1}, P, Q of the separator (row-major)
 template <int N>
 struct NdSmem {
-  alignas(16) double Wsp[N][GS];
+  alignas(16) double Wsp[N - 1][GS];  // stage k's at WSI(k) (the separator has none)
   alignas(16) double Sep[3][GS];
   double Part[3][12];  // the separator's three terms of an iteration (ph_sweep_nd)
 };
@@ -862,10 +865,10 @@ struct Smem {
   // per-wave partial reductions (32 per wave); during the sweeps the sink of lanes
   // whose store is void (lane (t & 31) + 12 j, j <= N/2 + 1)
   double red[(8 * kRows<N> + 32 > 12 * (N / 2 + 2) + 32) ? 8 * kRows<N> + 32 : 12 * (N / 2 + 2) + 32];
-  double dump[64];          // sink of predicated stores (never read): lane & 63
+  double dump[kND<N> ? 1 : 64];  // sink of predicated stores (never read): lane & 63 (kND: red[], as the sweeps')
   // (13 unused doubles: where round 4's deferred-check arrays sat; they keep every later
   // array's LDS offset, and with it the compiler's register allocation, as measured)
-  double pad13_[KI ? 1 : 13];
+  double pad13_[(KI || kND<N>) ? 1 : 13];
   alignas(16) double zero[72];  // zeros: masked coefficient reads point here instead of selecting
   // flag[4] (kXstLds): the ADMM loop's exit status, written by thread 0 at the (uniform)
   // exits and read by every thread after the loop
@@ -1808,7 +1811,7 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
             sync_all();
             nd_sweep_halves();
             sync_all();
-            if (cl && k != S) sh.nd.Wsp[k][RS * ph + cI] = sh.u.it.xs[XSL<N>(k)][ph];
+            if (cl && k != S) sh.nd.Wsp[WSI<N>(k)][RS * ph + cI] = sh.u.it.xs[XSL<N>(k)][ph];
           }
         }
         sync_all();
@@ -1821,8 +1824,8 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
           double Ro[12];
 #pragma unroll
           for (int ci = 0; ci < 12; ++ci) {
-            const double* const Wa = &sh.nd.Wsp[S - 1][0];
-            const double* const Wb = &sh.nd.Wsp[S + 1][0];
+            const double* const Wa = &sh.nd.Wsp[WSI<N>(S - 1)][0];
+            const double* const Wb = &sh.nd.Wsp[WSI<N>(S + 1)][0];
             double ga = cta * Wa[12 * ar + ci], gb = cba * Wb[12 * ar + ci];
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
@@ -1902,7 +1905,7 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
     if constexpr (ABG) zAb = Work<N>::ZERO - Work<N>::AB;
     else zAb = (int)(sh.zero - sh.Ab);
     lds_cd* XSr = (lds_cd*)&sh.u.it.xs[0][0];
-    double* const Wdump = &sh.dump[t & 63];
+    double* const Wdump = kND<N> ? &sh.red[t & 63] : &sh.dump[t & 63];  // (red: no reduction is live in ph_rhs)
     // The LDS offsets of the lane's coefficients, derived from its coordinates.  O0
     // is derived once and held (the loop phases up to 32 stages, where the ADMM loop
     // has the registers); a phase run between long stretches of other work -- the
@@ -2980,6 +2983,8 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
           const int wq = __builtin_amdgcn_readfirstlane(t >> 6);
           lds_d* const part = (lds_d*)&sh.nd.Part[0][0];  // [0]: P z_{S-1}, [1]: Q z_{S+1}, [2]: Sigma^{-1} b_S
           nd_sweep_halves();
+          STAMP(7);  // (diagnostic builds, kND: bucket 7 the outward sweep, 4 the separator terms, 5 the
+                     // barrier after them, 8 the correction; ph_recover's own wait joins bucket 7)
           if (wq < 2) {  // (the sweep's own wave_sync has published its states to the wave)
             // (lane ids from a laundered thread index: held across the loop, these addresses were
             // spilled and each reload waited for)
@@ -3002,23 +3007,26 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
               const dbl2 v = ((lds_cd2*)&sh.nd.Sep[0][RS * ph])[i];
               Si[2 * i] = v.x; Si[2 * i + 1] = v.y;
             }
-            const double bs = sh.u.it.bo[N - 1][ph] + sh.u.it.na[N - 1][ph];  // b_S (RSL: slot N-1)
+            const double bs = sh.u.it.bo[RSL<N>(S)][ph] + sh.u.it.na[RSL<N>(S)][ph];  // b_S
             const double sb = bdot_ln12(Si, bs, 0.0);
             if (cl) part[24 + ph] = sb;
           }
           if (pre) rec_pre(*pre);
+          STAMP(4);
           sync_all();  // z of both halves, the separator's three terms
+          STAMP(5);
           const double xv = (part[24 + ph] + part[ph]) + part[12 + ph];
           double Wr[12];
 #pragma unroll
           for (int i = 0; i < 6; ++i) {
-            const dbl2 v = ((lds_cd2*)&sh.nd.Wsp[k][RS * ph])[i];
+            const dbl2 v = ((lds_cd2*)&sh.nd.Wsp[WSI<N>(k == NDS<N> ? k - 1 : k)][RS * ph])[i];  // (the separator's product is unused)
             Wr[2 * i] = v.x; Wr[2 * i + 1] = v.y;
           }
           const double corr = bdot_ln12(Wr, xv, 0.0);
           double* const zk = &sh.u.it.xs[XSL<N>(k)][ph];
           const double zv = *zk;
           if (cl) *zk = k == S ? xv : zv - corr;
+          STAMP(8);
         }
       };
       // the state sweep: the lagging form up to 32 stages, the split form beyond

@@ -58,6 +58,8 @@ constexpr bool work_occ16(int) { return false; }
 // two-ended sweep at every horizon.
 #ifdef MPCQ_NO_ND
 constexpr bool nd_layout(int) { return false; }
+#elif defined(MPCQ_ND16)
+constexpr bool nd_layout(int N) { return N == 32 || N == 16; }  // (an experiment: N = 16 too)
 #else
 constexpr bool nd_layout(int N) { return N == 32; }
 #endif

@@ -28,6 +28,18 @@ NAMES_KI = list(NAMES)
 NAMES_KI[6] = "iter:Z r product (own share)"
 NAMES_KI[7] = "iter:product barrier wait"
 NAMES_KI[2] = "factor + Z formation"
+# the nested-dissection build (kND, N = 32): 15 ph_rhs + the barrier before the sweeps, 3 the
+# first rows, 6 the inward half sweep, 7 the outward half sweep (+ ph_recover's barrier wait),
+# 4 the separator's terms, 5 the barrier after them, 8 the correction (4 / 5 / 8 also take the
+# checks' publish / primal / dual phases, one iteration in 25)
+NAMES_ND = list(NAMES)
+NAMES_ND[15] = "nd:rhs + barrier"
+NAMES_ND[3] = "nd:first rows"
+NAMES_ND[6] = "nd:inward half sweep"
+NAMES_ND[7] = "nd:outward + recover wait"
+NAMES_ND[4] = "nd:sep terms (+chk)"
+NAMES_ND[5] = "nd:sep barrier (+chk)"
+NAMES_ND[8] = "nd:correction (+chk)"
 NAMES_CR = list(NAMES[:15]) + ["cr:reduce b + barrier"]
 NAMES_CR[3] = "iter:w,b,u,beta + barrier"
 NAMES_CR[7] = "cr:odd stages + barrier"
@@ -40,6 +52,7 @@ def main():
     ap.add_argument("--N", type=int, default=16)
     ap.add_argument("--cr", action="store_true", help="label the buckets of the cyclic-reduction build")
     ap.add_argument("--ki", action="store_true", help="label the buckets of the explicit-inverse build (N = 16)")
+    ap.add_argument("--nd", action="store_true", help="label the buckets of the nested-dissection build")
     ap.add_argument("--copies", type=int, default=-1,
                     help=">= 0: every instance a copy of this instance of the C2 batch (seed 2)")
     a = ap.parse_args()
@@ -64,7 +77,7 @@ def main():
     torch.cuda.synchronize()
     S = stamps.cpu().numpy().astype(np.float64)
     its = it.cpu().numpy()
-    names = NAMES_CR if a.cr else (NAMES_KI if a.ki else NAMES)
+    names = NAMES_CR if a.cr else (NAMES_KI if a.ki else (NAMES_ND if a.nd else NAMES))
     tot = S[:, :13].sum(axis=1) + S[:, 15]
     print(f"batch {a.batch} N={a.N}: iters median {np.median(its)} max {its.max()}; "
           f"kernel ms (event) {eng.last_kernel_ms()[1]:.2f}")

@@ -52,16 +52,17 @@ constexpr bool work_occ16(int N) { return N == 16 && MPCQ_OCC16 > 2; }
 #else
 constexpr bool work_occ16(int) { return false; }
 #endif
-// The nested-dissection state solve (mpcq_engine.hip kND, round 6): at these horizons the
-// scaled constraint values live in the workspace (72-double zero block + 126 N - 18, rounded
-// up to even), which frees the LDS for the separator's spikes.  -DMPCQ_NO_ND: the round-5
-// two-ended sweep at every horizon.
-#ifdef MPCQ_NO_ND
-constexpr bool nd_layout(int) { return false; }
-#elif defined(MPCQ_ND16)
-constexpr bool nd_layout(int N) { return N == 32 || N == 16; }  // (an experiment: N = 16 too)
-#else
+// The nested-dissection state solve (mpcq_engine.hip kND, round 6; an opt-in variant: measured
+// slower than the two-ended sweep): at these horizons the scaled
+// constraint values live in the workspace (72-double zero block + 126 N - 18, rounded up to
+// even), which frees the LDS for the separator's spikes.  -DMPCQ_ND: N = 32; -DMPCQ_ND16: N = 16
+// and 32.  Without either (the production build) the round-5 two-ended sweep at every horizon.
+#if defined(MPCQ_ND16)
+constexpr bool nd_layout(int N) { return N == 32 || N == 16; }
+#elif defined(MPCQ_ND)
 constexpr bool nd_layout(int N) { return N == 32; }
+#else
+constexpr bool nd_layout(int) { return false; }
 #endif
 constexpr int64_t work_doubles(int N) {
   if (nd_layout(N)) return 72 + ((126 * (int64_t)N - 18 + 1) & ~1);

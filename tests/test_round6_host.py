@@ -43,6 +43,7 @@ def test_nd_workspace_size_formula():
     scaled constraint values (126 N - 18, rounded up to even) -- mirrored from
     mpcq_internal.h (the engine static_asserts Work<N>::SIZE against it)."""
     src = open(os.path.join(REPO, "mpc-tsid_amd", "csrc", "mpcq_internal.h")).read()
-    m = re.search(r"constexpr bool nd_layout\(int N\) \{ return N == (\d+); \}", src)
+    m = re.search(r"#elif defined\(MPCQ_ND\)\nconstexpr bool nd_layout\(int N\) \{ return N == (\d+); \}", src)
     assert m and int(m.group(1)) == 32
+    assert "#else\nconstexpr bool nd_layout(int) { return false; }" in src  # the production build
     assert "if (nd_layout(N)) return 72 + ((126 * (int64_t)N - 18 + 1) & ~1);" in src

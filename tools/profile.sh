@@ -12,7 +12,9 @@ ARGS=${@:---config c2}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-B="python3 $R/bench.py $ARGS --steps 3 --warmup 1 --cpu-sample 0 --certify 0 --companion 0"
+# (no companion / reference25 / restatement: the counters would also count their launches of the
+# same kernel)
+B="python3 $R/bench.py $ARGS --steps 3 --warmup 1 --cpu-sample 0 --certify 0 --companion 0 --reference25 0 --restatement 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $B > $OUT/fetch.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $B > $OUT/write.log 2>&1 &&

@@ -1395,8 +1395,9 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
             return Mb + GS * jj;
           };
           STAMP(15);  // (diagnostic builds: as in ph_sweep_split)
-          if constexpr (ND) {
+          if constexpr (ND) {  // (the other waves pass their own barrier: nd_sweep_halves)
             row12(rowp(1));
+            sync_all();
           } else {
             if (t < 64) row12(rowp(1));
             sync_all();
@@ -1532,8 +1533,10 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
           }  // MPCQ_REP_SWEEP
       };
       // (kND) Both halves' sweeps, A on wave 0 and B on wave 1, one code path (B as an NDS-stage
-      // system with its phantom): the bases differ by a wave-uniform offset.  The caller has
-      // passed the barrier that publishes the right-hand sides.
+      // system with its phantom): the bases differ by a wave-uniform offset.  The barrier that
+      // publishes the right-hand sides is inside: the sweep waves read their first rows before
+      // theirs (as the whole-horizon sweep does), the other waves pass their own (a wave-uniform
+      // branch; every wave executes one s_barrier).
       auto nd_sweep_halves = [&]() __attribute__((always_inline)) {
         if constexpr (kND<N>) {
           constexpr int S = NDS<N>;
@@ -1543,6 +1546,8 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
             ph_sweep_lag(std::integral_constant<int, S>{}, std::integral_constant<int, 3>{}, std::true_type{},
                          (lds_cd*)&sh.u.it.bo[0][0] + o12, 12 * (N + 1), &sh.u.it.yv[0][0] + o12,
                          &sh.u.it.xs[0][0] + o12, GHr + og, (lds_cd*)&sh.Sm[0][0] + og);
+          } else {
+            sync_all();
           }
         }
       };
@@ -1808,8 +1813,7 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
               sh.u.it.na[RSL<N>(k)][ph] = 0.0;
               if (k == S) { sh.u.it.bo[kPhRhs<N>][ph] = 0.0; sh.u.it.na[kPhRhs<N>][ph] = 0.0; }
             }
-            sync_all();
-            nd_sweep_halves();
+            nd_sweep_halves();  // (its barrier publishes the right-hand sides)
             sync_all();
             if (cl && k != S) sh.nd.Wsp[WSI<N>(k)][RS * ph + cI] = sh.u.it.xs[XSL<N>(k)][ph];
           }
@@ -2979,7 +2983,6 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
       auto ph_sweep_nd = [&](RecPre* pre) __attribute__((always_inline)) {
         if constexpr (kND<N>) {
           constexpr int S = NDS<N>;
-          sync_all();  // the right-hand sides (ph_rhs)
           const int wq = __builtin_amdgcn_readfirstlane(t >> 6);
           lds_d* const part = (lds_d*)&sh.nd.Part[0][0];  // [0]: P z_{S-1}, [1]: Q z_{S+1}, [2]: Sigma^{-1} b_S
           nd_sweep_halves();
@@ -3012,16 +3015,18 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
             if (cl) part[24 + ph] = sb;
           }
           if (pre) rec_pre(*pre);
-          STAMP(4);
-          sync_all();  // z of both halves, the separator's three terms
-          STAMP(5);
-          const double xv = (part[24 + ph] + part[ph]) + part[12 + ph];
+          // this stage's spike row, read before the barrier (the waves that did not sweep have
+          // them in registers when it opens; after it, every wave's reads met in the LDS at once)
           double Wr[12];
 #pragma unroll
           for (int i = 0; i < 6; ++i) {
             const dbl2 v = ((lds_cd2*)&sh.nd.Wsp[WSI<N>(k == NDS<N> ? k - 1 : k)][RS * ph])[i];  // (the separator's product is unused)
             Wr[2 * i] = v.x; Wr[2 * i + 1] = v.y;
           }
+          STAMP(4);
+          sync_all();  // z of both halves, the separator's three terms
+          STAMP(5);
+          const double xv = (part[24 + ph] + part[ph]) + part[12 + ph];
           const double corr = bdot_ln12(Wr, xv, 0.0);
           double* const zk = &sh.u.it.xs[XSL<N>(k)][ph];
           const double zv = *zk;

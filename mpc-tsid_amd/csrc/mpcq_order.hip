@@ -59,30 +59,39 @@ __global__ __launch_bounds__(1024) void class_order_kernel(const int32_t* __rest
   __shared__ int cost[kSlots];          // bucket of each slot
   __shared__ int base[kBuckets];        // next free position of each bucket
   __shared__ int wcnt[kWaves][kBuckets];
-  __shared__ unsigned long long mean_all;
+  __shared__ unsigned long long tot_s, tot_n;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  if (t == 0) {
-    unsigned long long s = 0, n = 0;
-    for (int q = 0; q < kSlots; ++q) { s += sum[q]; n += cnt[q]; }
-    mean_all = n ? s / n : 0;
-  }
+  if (t == 0) { tot_s = 0; tot_n = 0; }
   if (t < kBuckets) base[t] = 0;
   __syncthreads();
+  unsigned long long my_s = 0, my_n = 0;
   if (t < kSlots) {
-    const unsigned long long e = cnt[t] ? sum[t] / cnt[t] : mean_all;
+    my_s = sum[t];
+    my_n = cnt[t];
+    if (my_n) { atomicAdd(&tot_s, my_s); atomicAdd(&tot_n, my_n); }
+  }
+  __syncthreads();
+  if (t < kSlots) {  // (the mean over every seen slot for a class not seen yet)
+    const unsigned long long e = my_n ? my_s / my_n : (tot_n ? tot_s / tot_n : 0);
     const unsigned long long q = e >> 4;
     cost[t] = q < kBuckets - 1 ? (int)q : kBuckets - 1;
   }
   __syncthreads();
   for (int64_t i = t; i < B; i += blockDim.x) atomicAdd(&base[cost[cls[i]]], 1);
   __syncthreads();
-  if (t == 0) {  // exclusive offsets, the most expensive bucket first
-    int acc = 0;
-    for (int q = kBuckets - 1; q >= 0; --q) {
-      const int h = base[q];
-      base[q] = acc;
-      acc += h;
+  if (w == 0) {  // exclusive offsets, the most expensive bucket first: four buckets per lane
+    int h[4], run = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { h[j] = base[kBuckets - 1 - (4 * lane + j)]; run += h[j]; }
+    int inc = run;  // inclusive scan of the lanes' sums
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o);
+      if (lane >= o) inc += v;
     }
+    int acc = inc - run;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { base[kBuckets - 1 - (4 * lane + j)] = acc; acc += h[j]; }
   }
   __syncthreads();
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -127,12 +136,26 @@ __global__ __launch_bounds__(256) void class_learn_kernel(const int32_t* __restr
                                                           const int32_t* __restrict__ iters, int64_t B,
                                                           unsigned long long* __restrict__ sum,
                                                           unsigned* __restrict__ cnt) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B) return;
-  const int32_t it = iters[i];
-  if (it <= 0) return;
-  atomicAdd(&sum[cls[i]], (unsigned long long)it);
-  atomicAdd(&cnt[cls[i]], 1u);
+  // a batch holds few classes: sum in LDS per block, then one global atomic per class and block
+  __shared__ unsigned long long bs[kSlots];
+  __shared__ unsigned bn[kSlots];
+  const int t = threadIdx.x;
+  for (int q = t; q < kSlots; q += blockDim.x) { bs[q] = 0; bn[q] = 0; }
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + t;
+  if (i < B) {
+    const int32_t it = iters[i];
+    if (it > 0) {
+      atomicAdd(&bs[cls[i]], (unsigned long long)it);
+      atomicAdd(&bn[cls[i]], 1u);
+    }
+  }
+  __syncthreads();
+  for (int q = t; q < kSlots; q += blockDim.x)
+    if (bn[q]) {
+      atomicAdd(&sum[q], bs[q]);
+      atomicAdd(&cnt[q], bn[q]);
+    }
 }
 
 }  // namespace

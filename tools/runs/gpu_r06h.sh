@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 # tick, the planner, and the 2-rank gloo rehearsal of the launcher -- same build as r06g (its
 # profiles/pmc_traffic.json committed before this call)
 O=gpurun_out
-T=r06h
+T=${T:-r06h}
 prof() {
   local tag=$1 key=$2 n=$3; shift 3
   bash tools/profile.sh $tag "$@" && python3 tools/prof_summary.py $tag --key $key --instances $n > $O/${tag}_summary.txt 2>&1

@@ -1,0 +1,23 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+# r06j: the final build (block-aggregated class learning, parallel class-order prologue) --
+# smoke, the whole GPU suite, then the stamped rocprofv3 passes of C2, C3 and the C4 / C5 rank
+# shards (tools/profile.sh, summarised on the box into profiles/pmc_traffic.json) and each bench
+# line after its profile
+O=gpurun_out
+T=r06j
+prof() {  # tag key instances bench-args...
+  local tag=$1 key=$2 n=$3; shift 3
+  bash tools/profile.sh $tag "$@" && python3 tools/prof_summary.py $tag --key $key --instances $n > $O/${tag}_summary.txt 2>&1
+}
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $O/${T}_smoke.log 2>&1 &&
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/${T}_pytest_gpu.log 2>&1 &&
+prof ${T} c2_N16_B1024 1024 --config c2 &&
+prof ${T}c3 c3_N32_B1024 1024 --config c3 &&
+prof ${T}c4s c4_N16_B8192 8192 --config c4 --batch 8192 &&
+prof ${T}c5s c5_N16_B4096 4096 --config c5 --batch 4096 &&
+timeout -k 10 300 python -u bench.py > $O/${T}_bench_c2.json 2> $O/${T}_bench_c2.err &&
+timeout -k 10 300 python -u bench.py --config c3 > $O/${T}_bench_c3.json 2> $O/${T}_bench_c3.err &&
+timeout -k 10 300 python -u bench.py --config c4 --batch 8192 --companion 0 --reference25 0 --cpu-sample 0 --certify 0 --restatement 512 > $O/${T}_bench_c4_shard8192.json 2> $O/${T}_bench_c4_shard.err &&
+timeout -k 10 300 python -u bench.py --config c5 --batch 4096 --companion 0 --reference25 0 --cpu-sample 0 --certify 0 --restatement 512 > $O/${T}_bench_c5_shard4096.json 2> $O/${T}_bench_c5_shard.err &&
+mkdir -p $O/profiles_${T} && cp profiles/${T}*_summary.md profiles/${T}*_kernel_stats.csv profiles/pmc_traffic.json $O/profiles_${T}/

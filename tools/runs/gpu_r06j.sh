@@ -1,7 +1,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-# r06j: the final build (block-aggregated class learning, parallel class-order prologue) --
-# smoke, the whole GPU suite, then the stamped rocprofv3 passes of C2, C3 and the C4 / C5 rank
+# r06j: the final build (block-aggregated class learning, parallel class-order prologue; the
+# check's reciprocals divided where used: scratch 240 -> 192 B per lane at N = 16) -- smoke, the
+# whole GPU suite, per-iteration times at N = 16 / 32, then the stamped rocprofv3 passes of C2, C3 and the C4 / C5 rank
 # shards (tools/profile.sh, summarised on the box into profiles/pmc_traffic.json) and each bench
 # line after its profile
 O=gpurun_out
@@ -12,6 +13,8 @@ prof() {  # tag key instances bench-args...
 }
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $O/${T}_smoke.log 2>&1 &&
 timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/${T}_pytest_gpu.log 2>&1 &&
+timeout -k 10 240 python -u tools/iterbench.py --N 16 --batches 256 > $O/${T}_iter16.txt 2>&1 &&
+timeout -k 10 240 python -u tools/iterbench.py --N 32 --batches 256 > $O/${T}_iter32.txt 2>&1 &&
 prof ${T} c2_N16_B1024 1024 --config c2 &&
 prof ${T}c3 c3_N32_B1024 1024 --config c3 &&
 prof ${T}c4s c4_N16_B8192 8192 --config c4 --batch 8192 &&

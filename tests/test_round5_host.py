@@ -119,7 +119,7 @@ def test_variant_and_stamps_builds_carry_their_own_stamp():
     finally:
         os.unlink(f.name)
     # the stamps library links mpcq_build_stamps.o (stamp + "+stamps"), not the production object
-    r = subprocess.run(["make", "-s", "-n", "-C", os.path.join(REPO, "mpc-tsid_amd", "csrc"), "../mpcq/libmpcq_stamps.so"],
+    r = subprocess.run(["make", "-s", "-n", "-B", "-C", os.path.join(REPO, "mpc-tsid_amd", "csrc"), "../mpcq/libmpcq_stamps.so"],
                        capture_output=True, text=True, timeout=120)
     link = [ln for ln in r.stdout.splitlines() if "-shared" in ln and "libmpcq_stamps.so" in ln]
     assert link and "mpcq_build_stamps.o" in link[-1] and "build/mpcq_build.o" not in link[-1]

@@ -36,3 +36,17 @@ def test_class_order_changes_no_result(N):
         walk = synth.make_batch(130, N, gaits=("bound",), seed=9)
         with mpcq.Engine(N) as e2:
             _same(_solve(e0, walk, False), _solve(e2, walk, True))
+
+
+def test_class_order_multi_chunk_batch():
+    """B > 1024: the order kernel ranks the batch in chunks of its 1024-thread workgroup, each
+    chunk's positions continuing the buckets' running offsets -- the dispatch must still be a
+    permutation (every instance solved once: outputs equal to the unordered solve's)."""
+    import mpcq
+    from mpcq import synth
+    syn = synth.make_batch(2600, 16, gaits=("trot", "bound", "pace"), seed=11)
+    with mpcq.Engine(16) as e0, mpcq.Engine(16) as e1:
+        ref = _solve(e0, syn, False)
+        assert np.isin(ref["status"], (1, 2)).all()
+        for _ in range(2):
+            _same(ref, _solve(e1, syn, True))

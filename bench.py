@@ -93,6 +93,10 @@ def parse():
                          "mean iteration count their gait class showed in the engine's earlier launches (the "
                          "warm-up ones first), the most expensive first; a one-gait batch keeps index order. "
                          "Scheduling only (results bit-identical); 0 = index order")
+    ap.add_argument("--slice", type=int, default=0,
+                    help="> 0: sliced solves (mpcq_set_slice, beyond 16 stages): each step runs as launches of up "
+                         "to SLICE ADMM iterations per instance, the suspended instances resumed until none is "
+                         "left (results bit-identical; the step's time spans all its slices); 0 = one launch")
     ap.add_argument("--rho-interval", type=int, default=0,
                     help="override adaptive_rho_interval (0 = the library default)")
     ap.add_argument("--cpu-sample", type=float, default=1.5,
@@ -519,6 +523,8 @@ def main():
             over["adaptive_rho_interval"] = args.rho_interval
         eng = mpcq.Engine(N, device=local, **over)
         eng.set_stream(stream.cuda_stream)
+        if args.slice > 0:
+            eng.set_slice(args.slice)
         f0_d = torch.empty((per, 12), dtype=torch.float64, device=dev)
         st_d = torch.empty(per, dtype=torch.int32, device=dev)
         it_d = torch.empty(per, dtype=torch.int32, device=dev)
@@ -661,7 +667,10 @@ def main():
                        "parallelism": f"shard{world}" + ("+gather" if args.gather else ""),
                        "dispatch": ("by gait class: the mean iteration count of each instance's class over the "
                                     "engine's earlier launches, most expensive first (MPCQ_FLAG_ORDER_BY_CLASS, in "
-                                    "the timed region)" if args.order_by_class else "index order")},
+                                    "the timed region)" if args.order_by_class else "index order")
+                                   + (f"; sliced: launches of up to {args.slice} ADMM iterations per instance, the "
+                                      "suspended ones resumed until none is left (mpcq_set_slice; every slice in the "
+                                      "timed region)" if args.slice > 0 and N > 16 else "")},
             "roofline": roof,
             "roofline_hbm": roof_hbm,
             "build": {"engine_src_sha": src_sha, "pmc_tag": pmc.get("tag"), "pmc_stale": pmc.get("stale")},

@@ -34,6 +34,17 @@ struct mpcq_ctx {
   uint32_t* cls_cnt = nullptr;
   int32_t* ord_buf = nullptr;
   int64_t ord_cap = 0;
+  // sliced solves (mpcq_set_slice): the slice length (0: off), the suspended instances'
+  // iterates (mpcq::res_lanes(N) x 8 doubles, rho, 4 counters each), two dispatch lists and a
+  // status scratch (3 B int32), the device / pinned-host count of the next slice
+  int32_t slice_iters = 0;
+  double* res = nullptr;
+  double* res_rho = nullptr;
+  int32_t* res_i = nullptr;
+  int32_t* sl_buf = nullptr;
+  int64_t sl_cap = 0;
+  int32_t* sl_count = nullptr;
+  int32_t* sl_host = nullptr;
 };
 
 namespace {
@@ -199,6 +210,43 @@ int check_ctx(mpcq_ctx* c, int64_t batch) {
   return MPCQ_OK;
 }
 
+// Sliced-solve scratch (mpcq_set_slice): the suspended iterates, the dispatch lists, the count
+int ensure_slice(mpcq_ctx* c, int64_t B) {
+  if (!c->sl_count) {
+    if (hipMalloc(&c->sl_count, 4) != hipSuccess) {
+      c->sl_count = nullptr;
+      return fail(MPCQ_E_NOMEM, "hipMalloc(4) for the slice count failed");
+    }
+    if (hipHostMalloc(&c->sl_host, 4, hipHostMallocDefault) != hipSuccess) {
+      c->sl_host = nullptr;
+      return fail(MPCQ_E_NOMEM, "hipHostMalloc(4) for the slice count failed");
+    }
+  }
+  if (B > c->sl_cap) {
+    if (c->res) {
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      HIP_TRY(hipFree(c->res));
+      HIP_TRY(hipFree(c->sl_buf));
+    }
+    c->res = nullptr;
+    c->sl_buf = nullptr;
+    c->sl_cap = 0;
+    const size_t rb = (size_t)B * (8 * (size_t)mpcq::res_lanes(c->N) + 1) * 8 + (size_t)B * 16;
+    if (hipMalloc(&c->res, rb) != hipSuccess) {
+      c->res = nullptr;
+      return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) for the suspended iterates failed", rb);
+    }
+    if (hipMalloc(&c->sl_buf, (size_t)B * 12) != hipSuccess) {
+      c->sl_buf = nullptr;
+      return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) for the slice lists failed", (size_t)B * 12);
+    }
+    c->res_rho = c->res + (size_t)B * 8 * (size_t)mpcq::res_lanes(c->N);
+    c->res_i = (int32_t*)(c->res_rho + B);
+    c->sl_cap = B;
+  }
+  return MPCQ_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -331,6 +379,10 @@ int mpcq_destroy(mpcq_ctx* c) {
   if (c->work) (void)hipFree(c->work);
   if (c->cls_sum) (void)hipFree(c->cls_sum);
   if (c->ord_buf) (void)hipFree(c->ord_buf);
+  if (c->res) (void)hipFree(c->res);
+  if (c->sl_buf) (void)hipFree(c->sl_buf);
+  if (c->sl_count) (void)hipFree(c->sl_count);
+  if (c->sl_host) (void)hipHostFree(c->sl_host);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -341,6 +393,13 @@ int mpcq_destroy(mpcq_ctx* c) {
 int mpcq_set_stream(mpcq_ctx* c, void* stream) {
   if (!c) return fail(MPCQ_E_INVALID, "ctx is NULL");
   c->stream = stream ? (hipStream_t)stream : c->own_stream;
+  return MPCQ_OK;
+}
+
+int mpcq_set_slice(mpcq_ctx* c, int32_t slice_iters) {
+  if (!c) return fail(MPCQ_E_INVALID, "ctx is NULL");
+  if (slice_iters < 0) return fail(MPCQ_E_INVALID, "slice_iters must be >= 0");
+  c->slice_iters = slice_iters;
   return MPCQ_OK;
 }
 
@@ -458,8 +517,42 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
     HIP_TRY(mpcq::launch_class_order(a.fsteps, B, cls, c->cls_sum, c->cls_cnt, order, c->stream));
     a.order = order;
   }
+  // sliced (mpcq_set_slice, beyond 16 stages): the first launch suspends every instance still
+  // running after slice_iters iterations; each further launch resumes the suspended ones, in
+  // the last launch's order, for another slice, until none is left (a count read back per slice)
+  const bool sliced = c->slice_iters > 0 && c->slice_iters < c->p.max_iter && N > 16;
+  if (sliced) {
+    rc = ensure_slice(c, B);
+    if (rc) return rc;
+    a.slice_iters = c->slice_iters;
+    a.res = c->res;
+    a.res_rho = c->res_rho;
+    a.res_i = c->res_i;
+    if (!a.status) a.status = c->sl_buf + 2 * B;  // (the slices' statuses; the caller asked for none)
+  }
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   HIP_TRY(mpcq::launch_solve(N, fused, c->p, a, c->stream));
+  if (sliced) {
+    const int32_t* prev = a.order;
+    int64_t cnt = B;
+    const int max_slices = c->p.max_iter / c->slice_iters + 2;
+    for (int sl = 0;; ++sl) {
+      if (sl > max_slices) return fail(MPCQ_E_DEVICE, "sliced solve: instances still suspended after %d slices", sl);
+      int32_t* list = c->sl_buf + (sl & 1) * B;
+      HIP_TRY(mpcq::launch_suspended(prev, cnt, a.status, list, c->sl_count, c->stream));
+      HIP_TRY(hipMemcpyAsync(c->sl_host, c->sl_count, 4, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      const int32_t left = *c->sl_host;
+      if (left <= 0) break;
+      mpcq::LaunchArgs r = a;
+      r.batch = left;
+      r.order = list;
+      r.resume = 1;
+      HIP_TRY(mpcq::launch_solve(N, fused, c->p, r, c->stream));
+      prev = list;
+      cnt = left;
+    }
+  }
   HIP_TRY(hipEventRecord(c->ev[3], c->stream));
   if (by_class) HIP_TRY(mpcq::launch_class_learn(cls, its, B, c->cls_sum, c->cls_cnt, c->stream));
   c->have_solve = true;

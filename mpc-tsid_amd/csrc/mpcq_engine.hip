@@ -108,6 +108,13 @@ __host__ __device__ constexpr int SIGX(int q) { return q <= N / 2 ? q : N + N / 
 // updates and the sums, and their maxima duplicate row N-1's.
 template <int N>
 constexpr int kRows = (N + 3) & ~3;
+// Sliced solves (LaunchArgs::slice_iters / resume, mpcq_set_slice) beyond 16 stages: one
+// instance per CU there, so a long solve dispatched in a late round ends the launch late
+// (DESIGN.md section 8).  Up to 16 stages two instances share a CU and slicing does not
+// shorten the modelled launch (section 8b item 9): the code is compiled out and the ADMM
+// loop's allocation stays the unsliced one.
+template <int N>
+constexpr bool kSlice = N > 16;
 
 // ---------------------------------------------------------------------------
 // cross-lane helpers
@@ -1178,8 +1185,10 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
 #ifdef MPCQ_FACTIME
     uint64_t fac_cycles = 0;
 #endif
-    double rho_s = a.rho_in ? a.rho_in[b] : p.rho;
+    // (a resumed slice: the rho and the update count it was suspended with)
+    double rho_s = kSlice<N> && a.resume ? a.res_rho[b] : (a.rho_in ? a.rho_in[b] : p.rho);
     rho_s = fmin(fmax(rho_s, kRhoMin), kRhoMax);
+    if (kSlice<N> && a.resume) n_upd = a.res_i[4 * b + 3];
 
     // per-row rho / 1/rho from the row's class and the (uniform) rho values
     double r_in = 0.0, r_eq = 0.0, ri_in = 0.0, ri_eq = 0.0;
@@ -2561,6 +2570,17 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
           y[j] = r >= 0 ? (p.dual_warm ? wy : cscale * wy / E[j]) : 0.0;
         }
       }
+      // a resumed slice (mpcq_set_slice): the iterate every lane held when it was suspended
+      if constexpr (kSlice<N> && !KI) {
+        if (a.resume) {
+          constexpr int64_t RL = res_lanes(N);
+          const double* const q = a.res + b * 8 * RL + t;
+          xf = q[0];
+          xX = q[RL];
+#pragma unroll
+          for (int j = 0; j < 3; ++j) { z[j] = q[(2 + j) * RL]; y[j] = q[(5 + j) * RL]; }
+        }
+      }
       sync_all();
       STAMP(1);
 
@@ -3442,6 +3462,16 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
         }
         kinv_admm(std::false_type{});
       } else {
+      // a resumed slice continues the saved loop counters; slice_iters > 0 suspends at the
+      // first segment end slice_iters iterations on (mpcq_set_slice)
+      if (kSlice<N> && a.resume) {
+        iter = __builtin_amdgcn_readfirstlane(a.res_i[4 * b]);
+        to_check = __builtin_amdgcn_readfirstlane(a.res_i[4 * b + 1]);
+        to_adapt = __builtin_amdgcn_readfirstlane(a.res_i[4 * b + 2]);
+      }
+      const int slice_end =
+          kSlice<N> && a.slice_iters > 0 && a.slice_iters < p.max_iter ? iter + a.slice_iters : 0x7fffffff;
+      bool suspended = false;
       // the bounds are re-derived where used (lo_of / hi_of: a select on the lane's
       // class and its row scaling in the fused path) rather than held in 6 registers
       for (;;) {
@@ -3563,8 +3593,29 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
           }
           STAMP(11);
           ++iter;
+          if (kSlice<N> && iter >= slice_end && iter <= p.max_iter) {  // (uniform) suspend this slice here
+            suspended = true;
+            break;
+          }
         }
         if (!refactor) break;
+      }
+      if (kSlice<N> && suspended) {  // the iterate and the loop's counters for the next slice; no other output
+        constexpr int64_t RL = res_lanes(N);
+        double* const q = a.res + b * 8 * RL + t;
+        q[0] = xf;
+        q[RL] = xX;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) { q[(2 + j) * RL] = z[j]; q[(5 + j) * RL] = y[j]; }
+        if (t == 0) {
+          a.res_rho[b] = rho_s;
+          a.res_i[4 * b] = iter;
+          a.res_i[4 * b + 1] = to_check;
+          a.res_i[4 * b + 2] = to_adapt;
+          a.res_i[4 * b + 3] = n_upd;
+          if (a.status) a.status[b] = kStatusSuspended;
+        }
+        return;
       }
       if constexpr (kXstLds<N>) {
         sync_all();  // thread 0's exit status

@@ -33,7 +33,20 @@ struct LaunchArgs {
   uint64_t* stamps;    // [B][16] diagnostic build only (MPCQ_STAMPS): cycles per phase
   double* work;        // [B][work_doubles(N)] engine workspace (N > 32 and the nested-dissection horizons)
   const int32_t* order; // [B] instance solved by workgroup i (a permutation of 0..B-1), or null: i
+  // sliced solves (mpcq_set_slice): slice_iters > 0 suspends an instance at the first segment
+  // end (a check / adaptive-rho / max_iter boundary of the ADMM loop) after slice_iters more
+  // iterations: its iterate and loop counters to res / res_rho / res_i, status
+  // kStatusSuspended, no other output.  resume != 0: every instance of this launch starts from
+  // its saved iterate (the formulation, scaling and factorisation at the saved rho recomputed:
+  // the same bits) instead of the cold point.
+  int32_t slice_iters;
+  int32_t resume;
+  double* res;          // [B][8][res_lanes(N)]: xf, xX, z[3], y[3] of every lane
+  double* res_rho;      // [B]
+  int32_t* res_i;       // [B][4]: next iteration, to the next check, to the next adaptation, rho updates
 };
+constexpr int32_t kStatusSuspended = 100;  // (internal: the host loop resumes these)
+constexpr int64_t res_lanes(int N) { return 16 * (int64_t)((N + 3) & ~3); }
 
 // Doubles of engine workspace per instance: 0 up to 32 stages (everything in LDS);
 // beyond, a 288-double pad, S^{-1} (N x 144 + 2), F W (N x 72), R^{-1} Q (N x 36),
@@ -131,6 +144,10 @@ hipError_t launch_class_order(const double* fsteps, int64_t batch, int32_t* cls,
                               const uint32_t* cnt, int32_t* order, hipStream_t s);
 hipError_t launch_class_learn(const int32_t* cls, const int32_t* iters, int64_t batch, uint64_t* sum,
                               uint32_t* cnt, hipStream_t s);
+// Sliced solves: list[*count] = the instances of prev[0..n) (null: 0..n-1) whose status is
+// kStatusSuspended, in that order (one workgroup, stable).
+hipError_t launch_suspended(const int32_t* prev, int64_t n, const int32_t* status, int32_t* list,
+                            int32_t* count, hipStream_t s);
 
 // Launchers (mpcq_engine.hip).  Return hipError_t.
 hipError_t launch_formulate(int N, const mpcq_params& p, const LaunchArgs& a, hipStream_t s);

@@ -19,6 +19,8 @@
 //   class_learn_kernel: after the engine, each instance's iteration count into its slot.
 // Every instance's result is independent of the workgroup that solves it, so the order
 // changes no result bit (tests/test_gpu_order.py).
+// suspended_kernel (sliced solves, mpcq_set_slice): the instances a launch suspended, in its
+// order, for the next launch.
 #include <stdint.h>
 
 #include "mpcq_internal.h"
@@ -158,9 +160,52 @@ __global__ __launch_bounds__(256) void class_learn_kernel(const int32_t* __restr
     }
 }
 
+// Sliced solves (mpcq_set_slice): the suspended instances of the last launch, in its
+// dispatch order, for the next one (a stable compaction by wave ballots, one workgroup)
+__global__ __launch_bounds__(1024) void suspended_kernel(const int32_t* __restrict__ prev, int64_t n,
+                                                         const int32_t* __restrict__ status,
+                                                         int32_t* __restrict__ list, int32_t* __restrict__ count) {
+  __shared__ int wsum[kWaves];
+  __shared__ int base;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  if (t == 0) base = 0;
+  __syncthreads();
+  for (int64_t c0 = 0; c0 < n; c0 += blockDim.x) {
+    const int64_t i = c0 + t;
+    int32_t id = -1;
+    bool sus = false;
+    if (i < n) {
+      id = prev ? prev[i] : (int32_t)i;
+      sus = status[id] == kStatusSuspended;
+    }
+    const unsigned long long m = __ballot(sus);
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    int off = base;
+    for (int v = 0; v < w; ++v) off += wsum[v];
+    if (sus) list[off + __popcll(m & below)] = id;
+    __syncthreads();
+    if (t == 0) {
+      int tot = 0;
+      for (int v = 0; v < kWaves; ++v) tot += wsum[v];
+      base += tot;
+    }
+    __syncthreads();
+  }
+  if (t == 0) *count = base;
+}
+
 }  // namespace
 
 int class_table_slots() { return kSlots; }
+
+hipError_t launch_suspended(const int32_t* prev, int64_t n, const int32_t* status, int32_t* list,
+                            int32_t* count, hipStream_t s) {
+  if (n <= 0 || n > INT32_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(suspended_kernel, dim3(1), dim3(1024), 0, s, prev, n, status, list, count);
+  return hipGetLastError();
+}
 
 hipError_t launch_class_order(const double* fsteps, int64_t B, int32_t* cls, const uint64_t* sum,
                               const uint32_t* cnt, int32_t* order, hipStream_t s) {

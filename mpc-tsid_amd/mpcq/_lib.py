@@ -63,7 +63,7 @@ SV_ORDER = 16  # read-only: the next tick's dispatch order
 
 EXPORTS = ("mpcq_abi_version", "mpcq_default_params", "mpcq_dims", "mpcq_pattern",
            "mpcq_supported_horizons", "mpcq_last_error", "mpcq_create", "mpcq_destroy",
-           "mpcq_set_stream", "mpcq_last_kernel_ms", "mpcq_formulate_batch",
+           "mpcq_set_stream", "mpcq_set_slice", "mpcq_last_kernel_ms", "mpcq_formulate_batch",
            "mpcq_qp_solve_batch", "mpcq_solve_batch", "mpcq_default_planner_params",
            "mpcq_plan_batch", "mpcq_session_create", "mpcq_session_destroy", "mpcq_session_tick",
            "mpcq_session_read", "mpcq_session_write", "mpcq_session_device_ptr", "mpcq_debug_set_stamps",
@@ -194,6 +194,7 @@ def lib():
     L.mpcq_create.argtypes = [C.c_int, C.c_int, PP, C.POINTER(vp)]
     L.mpcq_destroy.argtypes = [vp]
     L.mpcq_set_stream.argtypes = [vp, vp]
+    L.mpcq_set_slice.argtypes = [vp, C.c_int32]
     L.mpcq_last_kernel_ms.argtypes = [vp, dp, dp]
     L.mpcq_formulate_batch.argtypes = [vp, C.c_int64, vp, vp, C.c_int, vp, vp, vp, vp, C.c_uint32]
     L.mpcq_qp_solve_batch.argtypes = [vp, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
@@ -211,7 +212,7 @@ def lib():
     L.mpcq_session_device_ptr.argtypes = [vp, C.c_int, C.POINTER(vp)]
     L.mpcq_plan_batch.argtypes = [vp, C.POINTER(PlannerParams), C.c_int64, C.c_uint32, C.c_int] + [vp] * 12 + [C.c_uint32]
     for name in ("mpcq_dims", "mpcq_pattern", "mpcq_supported_horizons", "mpcq_create",
-                 "mpcq_destroy", "mpcq_set_stream", "mpcq_last_kernel_ms", "mpcq_formulate_batch",
+                 "mpcq_destroy", "mpcq_set_stream", "mpcq_set_slice", "mpcq_last_kernel_ms", "mpcq_formulate_batch",
                  "mpcq_qp_solve_batch", "mpcq_solve_batch", "mpcq_default_planner_params",
            "mpcq_plan_batch", "mpcq_session_create", "mpcq_session_destroy", "mpcq_session_tick",
            "mpcq_session_read", "mpcq_session_write", "mpcq_session_device_ptr", "mpcq_debug_set_stamps"):

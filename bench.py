@@ -93,10 +93,12 @@ def parse():
                          "mean iteration count their gait class showed in the engine's earlier launches (the "
                          "warm-up ones first), the most expensive first; a one-gait batch keeps index order. "
                          "Scheduling only (results bit-identical); 0 = index order")
-    ap.add_argument("--slice", type=int, default=0,
+    ap.add_argument("--slice", type=int, default=-1,
                     help="> 0: sliced solves (mpcq_set_slice, beyond 16 stages): each step runs as launches of up "
                          "to SLICE ADMM iterations per instance, the suspended instances resumed until none is "
-                         "left (results bit-identical; the step's time spans all its slices); 0 = one launch")
+                         "left (results bit-identical; the step's time spans all its slices); 0 = one launch; "
+                         f"-1 (default) = {AUTO_SLICE} beyond 16 stages (C3: the best of 400-2800 measured, "
+                         "profiles/r06m_bench_c3_s*.json, r06n_bench_c3_s*.json), 0 up to 16")
     ap.add_argument("--rho-interval", type=int, default=0,
                     help="override adaptive_rho_interval (0 = the library default)")
     ap.add_argument("--cpu-sample", type=float, default=1.5,
@@ -116,6 +118,9 @@ def parse():
                          "FootstepPlanner kernel alone; tick: closed-loop sessions (planner + warm-started "
                          "solve + retrieve per robot and tick, virtual robot)")
     return ap.parse_args()
+
+
+AUTO_SLICE = 1600  # bench.py --slice -1 beyond 16 stages
 
 
 def load_pmc(tag: str, src_sha: str | None = None, path: str | None = None) -> dict:
@@ -493,6 +498,8 @@ def main():
 
     cfg = CONFIGS[args.config]
     N = cfg["N"]
+    if args.slice < 0:  # (auto) sliced beyond 16 stages: one instance per CU there
+        args.slice = AUTO_SLICE if N > 16 else 0
     if args.batch > 0:
         total = args.batch * world
     elif cfg["per_gpu"]:
@@ -623,7 +630,8 @@ def main():
         # QP instances solved (status 1 solved / 2 solved inaccurate) by all ranks per second
         value = float(allst[:, 0].sum()) * args.steps / wall_max
         fl0, by0 = float(allst[0, 2]), float(allst[0, 3])
-        tag = f"{args.config}_N{N}_B{per}" + ("_polish" if pol else "")
+        tag = (f"{args.config}_N{N}_B{per}" + ("_polish" if pol else "")
+               + (f"_s{args.slice}" if args.slice > 0 and N > 16 else ""))
         src_sha = lib_sha()
         pmc = load_pmc(tag, src_sha)
         roof = {"bound": "valu_fp64", "achieved": fl0 / (kern_ms * 1e-3) / 1e12, "peak": PEAK_FP64_TFLOPS,

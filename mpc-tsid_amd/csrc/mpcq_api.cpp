@@ -520,7 +520,7 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
   // sliced (mpcq_set_slice, beyond 16 stages): the first launch suspends every instance still
   // running after slice_iters iterations; each further launch resumes the suspended ones, in
   // the last launch's order, for another slice, until none is left (a count read back per slice)
-  const bool sliced = c->slice_iters > 0 && c->slice_iters < c->p.max_iter && N > 16;
+  const bool sliced = c->slice_iters > 0 && c->slice_iters < c->p.max_iter && (N > 16 || getenv("MPCQ_SLICE16"));
   if (sliced) {
     rc = ensure_slice(c, B);
     if (rc) return rc;

@@ -113,8 +113,13 @@ constexpr int kRows = (N + 3) & ~3;
 // (DESIGN.md section 8).  Up to 16 stages two instances share a CU and slicing does not
 // shorten the modelled launch (section 8b item 9): the code is compiled out and the ADMM
 // loop's allocation stays the unsliced one.
+// (-DMPCQ_SLICE16: at every horizon -- an experiment)
 template <int N>
+#ifdef MPCQ_SLICE16
+constexpr bool kSlice = true;
+#else
 constexpr bool kSlice = N > 16;
+#endif
 
 // ---------------------------------------------------------------------------
 // cross-lane helpers

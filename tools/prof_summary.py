@@ -53,10 +53,6 @@ def bench_stamp(logpath):
     return None
 
 
-def mean(v):
-    return sum(v) / len(v) if v else None
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
@@ -81,9 +77,18 @@ def main():
         if k2 != "SQ_WAVES":
             sq[k2] = v2
     f64 = counters(os.path.join(src, "f64", "run_counter_collection.csv"), a.kernel)
-    # the counter passes replay the same launches: their kernel time is the trace's average
-    kern_ms = (sum(float(r["AverageNs"]) * int(r["Calls"]) for r in eng) /
-               max(1, sum(int(r["Calls"]) for r in eng)) / 1e6) if eng else None
+    # figures per solve: a sliced solve (mpcq_set_slice) is its first launch (the whole batch's
+    # grid) and the resumed launches after it (smaller grids); unsliced, a solve is one launch.
+    # The counter passes replay the same launches: their kernel time is the trace's.
+    grids = [int(r["Grid_Size_X"]) for r in trace]
+    solves = sum(1 for g in grids if g == max(grids)) if grids else 0
+    dispatches = len(trace)
+    if not solves:
+        solves = max(1, sum(int(r["Calls"]) for r in eng))
+    kern_ms = (sum(float(r["AverageNs"]) * int(r["Calls"]) for r in eng) / solves / 1e6) if eng else None
+
+    def mean(v):  # (per solve: the sum over its launches; one launch each when unsliced)
+        return sum(v) / solves if v else None
 
     # every pass must have run the same build; the stamp goes into pmc_traffic.json, and
     # bench.py drops an entry whose stamp differs from the library it is running
@@ -100,6 +105,10 @@ def main():
     traffic = None
     lines = [f"# rocprofv3 summary `{a.tag}` ({a.key})", "",
              f"- build: libmpcq.so engine_src_sha `{sha}` (mpcq_build_info of the profiled process, every pass)"]
+    if dispatches > solves:
+        lines.append(f"- sliced solves: {dispatches} engine launches for {solves} solves (the first slice's grid "
+                     f"{max(grids)} threads, the resumed slices' smaller); the kernel time, counters and traffic below "
+                     f"are per solve (the sum over its slices): {kern_ms:.3f} ms")
     for r in eng:
         lines.append(f"- kernel `{r['Name']}`: {r['Calls']} calls, average {float(r['AverageNs']) / 1e6:.3f} ms "
                      f"(min {float(r['MinNs']) / 1e6:.3f}, max {float(r['MaxNs']) / 1e6:.3f}), "
@@ -177,6 +186,7 @@ def main():
         d[a.key] = {"bytes_per_launch": traffic, "fetch_kib": fk, "write_kib": wk, "tag": a.tag,
                     "engine_src_sha": sha,
                     "fp64_flops_per_launch": fp64_flops, "kernel_ms": kern_ms,
+                    "launches_per_solve": dispatches / solves if solves else None,
                     "note": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section), separate --pmc passes; "
                             "fp64 flops = (2 SQ_INSTS_VALU_FMA_F64 + ADD_F64 + MUL_F64) x 64 from their own pass"}
         json.dump(d, open(path, "w"), indent=1)

@@ -40,6 +40,7 @@ struct mpcq_ctx {
   int32_t slice_iters = 0;
   double* res = nullptr;
   double* res_rho = nullptr;
+  double* res_key = nullptr;
   int32_t* res_i = nullptr;
   int32_t* sl_buf = nullptr;
   int64_t sl_cap = 0;
@@ -231,7 +232,7 @@ int ensure_slice(mpcq_ctx* c, int64_t B) {
     c->res = nullptr;
     c->sl_buf = nullptr;
     c->sl_cap = 0;
-    const size_t rb = (size_t)B * (8 * (size_t)mpcq::res_lanes(c->N) + 1) * 8 + (size_t)B * 16;
+    const size_t rb = (size_t)B * (8 * (size_t)mpcq::res_lanes(c->N) + 2) * 8 + (size_t)B * 16;
     if (hipMalloc(&c->res, rb) != hipSuccess) {
       c->res = nullptr;
       return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) for the suspended iterates failed", rb);
@@ -241,7 +242,8 @@ int ensure_slice(mpcq_ctx* c, int64_t B) {
       return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) for the slice lists failed", (size_t)B * 12);
     }
     c->res_rho = c->res + (size_t)B * 8 * (size_t)mpcq::res_lanes(c->N);
-    c->res_i = (int32_t*)(c->res_rho + B);
+    c->res_key = c->res_rho + B;
+    c->res_i = (int32_t*)(c->res_key + B);
     c->sl_cap = B;
   }
   return MPCQ_OK;
@@ -518,8 +520,9 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
     a.order = order;
   }
   // sliced (mpcq_set_slice, beyond 16 stages): the first launch suspends every instance still
-  // running after slice_iters iterations; each further launch resumes the suspended ones, in
-  // the last launch's order, for another slice, until none is left (a count read back per slice)
+  // running after slice_iters iterations; each further launch resumes the suspended ones, the
+  // farthest from convergence (primal residual / tolerance) first, for another slice, until none
+  // is left (a count read back per slice)
   const bool sliced = c->slice_iters > 0 && c->slice_iters < c->p.max_iter && (N > 16 || getenv("MPCQ_SLICE16"));
   if (sliced) {
     rc = ensure_slice(c, B);
@@ -527,6 +530,7 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
     a.slice_iters = c->slice_iters;
     a.res = c->res;
     a.res_rho = c->res_rho;
+    a.res_key = c->res_key;
     a.res_i = c->res_i;
     if (!a.status) a.status = c->sl_buf + 2 * B;  // (the slices' statuses; the caller asked for none)
   }
@@ -539,7 +543,7 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
     for (int sl = 0;; ++sl) {
       if (sl > max_slices) return fail(MPCQ_E_DEVICE, "sliced solve: instances still suspended after %d slices", sl);
       int32_t* list = c->sl_buf + (sl & 1) * B;
-      HIP_TRY(mpcq::launch_suspended(prev, cnt, a.status, list, c->sl_count, c->stream));
+      HIP_TRY(mpcq::launch_suspended(prev, cnt, a.status, c->res_key, list, c->sl_count, c->stream));
       HIP_TRY(hipMemcpyAsync(c->sl_host, c->sl_count, 4, hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
       const int32_t left = *c->sl_host;

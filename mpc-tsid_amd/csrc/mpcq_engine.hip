@@ -3614,6 +3614,7 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
         for (int j = 0; j < 3; ++j) { q[(2 + j) * RL] = z[j]; q[(5 + j) * RL] = y[j]; }
         if (t == 0) {
           a.res_rho[b] = rho_s;
+          a.res_key[b] = pri_res / eps_pri;  // (the last segment end's update_info)
           a.res_i[4 * b] = iter;
           a.res_i[4 * b + 1] = to_check;
           a.res_i[4 * b + 2] = to_adapt;

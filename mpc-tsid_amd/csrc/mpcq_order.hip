@@ -19,8 +19,8 @@
 //   class_learn_kernel: after the engine, each instance's iteration count into its slot.
 // Every instance's result is independent of the workgroup that solves it, so the order
 // changes no result bit (tests/test_gpu_order.py).
-// suspended_kernel (sliced solves, mpcq_set_slice): the instances a launch suspended, in its
-// order, for the next launch.
+// suspended_kernel (sliced solves, mpcq_set_slice): the instances a launch suspended, the
+// farthest from convergence first, for the next launch.
 #include <stdint.h>
 
 #include "mpcq_internal.h"
@@ -160,50 +160,97 @@ __global__ __launch_bounds__(256) void class_learn_kernel(const int32_t* __restr
     }
 }
 
-// Sliced solves (mpcq_set_slice): the suspended instances of the last launch, in its
-// dispatch order, for the next one (a stable compaction by wave ballots, one workgroup)
+// Sliced solves (mpcq_set_slice): the suspended instances of the last launch for the next one,
+// the largest key first -- the primal residual over its tolerance when the instance was
+// suspended, which ranks the remaining work (Spearman +0.98 with the final iteration count over
+// C3's instances suspended at 1600 iterations) -- in buckets of 1/8 octave, the last launch's
+// order inside a bucket: a stable counting sort in one workgroup (the class order's scheme)
+__device__ __forceinline__ int key_bucket(double v) {
+  if (!(v > 0.0)) return 0;
+  const double e = floor(8.0 * log2(v)) + 128.0;  // (1/8 octave; keys from 2^-16 to 2^16)
+  return e < 0.0 ? 0 : (e > kBuckets - 1.0 ? kBuckets - 1 : (int)e);
+}
+
 __global__ __launch_bounds__(1024) void suspended_kernel(const int32_t* __restrict__ prev, int64_t n,
                                                          const int32_t* __restrict__ status,
+                                                         const double* __restrict__ key,
                                                          int32_t* __restrict__ list, int32_t* __restrict__ count) {
-  __shared__ int wsum[kWaves];
-  __shared__ int base;
+  __shared__ int base[kBuckets];
+  __shared__ int wcnt[kWaves][kBuckets];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const unsigned long long below = (1ull << lane) - 1ull;
-  if (t == 0) base = 0;
+  if (t < kBuckets) base[t] = 0;
+  __syncthreads();
+  for (int64_t i = t; i < n; i += blockDim.x) {
+    const int32_t id = prev ? prev[i] : (int32_t)i;
+    if (status[id] == kStatusSuspended) atomicAdd(&base[key_bucket(key[id])], 1);
+  }
+  __syncthreads();
+  if (w == 0) {  // exclusive offsets, the largest key first (four buckets per lane)
+    int h[4], run = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { h[j] = base[kBuckets - 1 - (4 * lane + j)]; run += h[j]; }
+    int inc = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o);
+      if (lane >= o) inc += v;
+    }
+    if (lane == 63) *count = inc;  // (the total)
+    int acc = inc - run;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { base[kBuckets - 1 - (4 * lane + j)] = acc; acc += h[j]; }
+  }
   __syncthreads();
   for (int64_t c0 = 0; c0 < n; c0 += blockDim.x) {
+    for (int e = t; e < kWaves * kBuckets; e += blockDim.x) (&wcnt[0][0])[e] = 0;
+    __syncthreads();
     const int64_t i = c0 + t;
     int32_t id = -1;
-    bool sus = false;
+    int q = -1;
     if (i < n) {
       id = prev ? prev[i] : (int32_t)i;
-      sus = status[id] == kStatusSuspended;
+      if (status[id] == kStatusSuspended) q = key_bucket(key[id]);
     }
-    const unsigned long long m = __ballot(sus);
-    if (lane == 0) wsum[w] = __popcll(m);
-    __syncthreads();
-    int off = base;
-    for (int v = 0; v < w; ++v) off += wsum[v];
-    if (sus) list[off + __popcll(m & below)] = id;
-    __syncthreads();
-    if (t == 0) {
-      int tot = 0;
-      for (int v = 0; v < kWaves; ++v) tot += wsum[v];
-      base += tot;
+    int rank = 0;
+    bool done = q < 0;
+    for (;;) {
+      const unsigned long long pend = __ballot(!done);
+      if (!pend) break;
+      const int leader = __ffsll((long long)pend) - 1;
+      const int ql = __shfl(q, leader);
+      const unsigned long long m = __ballot(!done && q == ql);
+      if (!done && q == ql) {
+        rank = __popcll(m & below);
+        done = true;
+      }
+      if (lane == leader) wcnt[w][ql] = __popcll(m);
     }
+    __syncthreads();
+    if (t < kBuckets) {
+      int run = base[t];
+#pragma unroll
+      for (int v = 0; v < kWaves; ++v) {
+        const int h = wcnt[v][t];
+        wcnt[v][t] = run;
+        run += h;
+      }
+      base[t] = run;
+    }
+    __syncthreads();
+    if (q >= 0) list[wcnt[w][q] + rank] = id;
     __syncthreads();
   }
-  if (t == 0) *count = base;
 }
 
 }  // namespace
 
 int class_table_slots() { return kSlots; }
 
-hipError_t launch_suspended(const int32_t* prev, int64_t n, const int32_t* status, int32_t* list,
-                            int32_t* count, hipStream_t s) {
+hipError_t launch_suspended(const int32_t* prev, int64_t n, const int32_t* status, const double* key,
+                            int32_t* list, int32_t* count, hipStream_t s) {
   if (n <= 0 || n > INT32_MAX) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(suspended_kernel, dim3(1), dim3(1024), 0, s, prev, n, status, list, count);
+  hipLaunchKernelGGL(suspended_kernel, dim3(1), dim3(1024), 0, s, prev, n, status, key, list, count);
   return hipGetLastError();
 }
 

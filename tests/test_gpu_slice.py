@@ -89,3 +89,11 @@ def test_slice_is_a_no_op_at_16_stages():
     from mpcq import synth
     syn = synth.make_batch(200, 16, gaits=("trot",), seed=2)
     _pair(16, syn, (25,))
+
+
+def test_slices_multi_chunk_compaction():
+    """More instances than the compaction's 1024-thread workgroup: the suspended ones are ranked
+    in chunks (the residual-key counting sort's running offsets) -- still every instance once."""
+    from mpcq import synth
+    syn = synth.make_batch(2100, 20, gaits=("trot", "bound"), seed=6)
+    _pair(20, syn, (60,))

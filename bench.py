@@ -94,11 +94,12 @@ def parse():
                          "warm-up ones first), the most expensive first; a one-gait batch keeps index order. "
                          "Scheduling only (results bit-identical); 0 = index order")
     ap.add_argument("--slice", type=int, default=-1,
-                    help="> 0: sliced solves (mpcq_set_slice, beyond 16 stages): each step runs as launches of up "
-                         "to SLICE ADMM iterations per instance, the suspended instances resumed until none is "
-                         "left (results bit-identical; the step's time spans all its slices); 0 = one launch; "
-                         f"-1 (default) = {AUTO_SLICE} beyond 16 stages (C3: the best of 400-2800 measured, "
-                         "profiles/r06m_bench_c3_s*.json, r06n_bench_c3_s*.json), 0 up to 16")
+                    help="> 0: sliced solves (mpcq_set_slice, beyond 16 stages): each step's first launch "
+                         "suspends the instances still iterating after SLICE ADMM iterations, a second launch "
+                         "resumes them, the farthest from convergence first, to their end (results bit-identical; "
+                         "the step's time spans both launches); 0 = one launch; "
+                         f"-1 (default) = {AUTO_SLICE} beyond 16 stages (C3's best measured, "
+                         "profiles/r06*_bench_c3_*s*.json), 0 up to 16")
     ap.add_argument("--rho-interval", type=int, default=0,
                     help="override adaptive_rho_interval (0 = the library default)")
     ap.add_argument("--cpu-sample", type=float, default=1.5,
@@ -676,9 +677,10 @@ def main():
                        "dispatch": ("by gait class: the mean iteration count of each instance's class over the "
                                     "engine's earlier launches, most expensive first (MPCQ_FLAG_ORDER_BY_CLASS, in "
                                     "the timed region)" if args.order_by_class else "index order")
-                                   + (f"; sliced: launches of up to {args.slice} ADMM iterations per instance, the "
-                                      "suspended ones resumed until none is left (mpcq_set_slice; every slice in the "
-                                      "timed region)" if args.slice > 0 and N > 16 else "")},
+                                   + (f"; sliced: the instances still iterating after {args.slice} ADMM iterations "
+                                      "suspended and resumed in a second launch, the farthest from convergence first "
+                                      "(mpcq_set_slice; both launches in the timed region)"
+                                      if args.slice > 0 and N > 16 else "")},
             "roofline": roof,
             "roofline_hbm": roof_hbm,
             "build": {"engine_src_sha": src_sha, "pmc_tag": pmc.get("tag"), "pmc_stale": pmc.get("stale")},

@@ -154,15 +154,16 @@ int mpcq_set_stream(mpcq_ctx* ctx, void* stream);
 int mpcq_last_kernel_ms(mpcq_ctx* ctx, double* formulate_ms, double* solve_ms);
 /* Sliced batch solves (no reference counterpart: a dispatch policy, no result changes).
  * slice_iters > 0: beyond 16 stages, the batch solves of this context (mpcq_solve_batch,
- * mpcq_qp_solve_batch) run as a sequence of launches: the first suspends every instance still
- * iterating at the first ADMM segment end (check / adaptive-rho / max_iter boundary) after
- * slice_iters iterations and saves its iterate in device scratch; each further launch resumes
- * the suspended ones (formulation, scaling and the factorisation at the saved rho recomputed)
- * for another slice, until none is left.  Every output is bit-identical to the unsliced
- * solve's; long instances no longer hold a CU slot past the others, so a batch whose instances
- * fill the CUs in several rounds ends sooner.  The host reads one count
- * back per slice (the call synchronises ctx's stream between slices).  0 (the default), a
- * slice of max_iter or more, and horizons up to 16: one launch. */
+ * mpcq_qp_solve_batch) run as two launches: the first suspends every instance still iterating
+ * at the first ADMM segment end (check / adaptive-rho / max_iter boundary) after slice_iters
+ * iterations and saves its iterate in device scratch; the second resumes the suspended ones
+ * (formulation, scaling and the factorisation at the saved rho recomputed), the farthest from
+ * convergence (primal residual over its tolerance) first, and runs them to their end.  Every
+ * output is bit-identical to the unsliced solve's; long instances no longer hold a CU slot
+ * past the others and start first once known, so a batch whose instances fill the CUs in
+ * several rounds ends sooner.  The host reads one count back between
+ * the launches (the call synchronises ctx's stream there).  0 (the default), a slice of
+ * max_iter or more, and horizons up to 16: one launch. */
 int mpcq_set_slice(mpcq_ctx* ctx, int32_t slice_iters);
 
 /* ---- formulation -----------------------------------------------------------

@@ -35,8 +35,9 @@ struct mpcq_ctx {
   int32_t* ord_buf = nullptr;
   int64_t ord_cap = 0;
   // sliced solves (mpcq_set_slice): the slice length (0: off), the suspended instances'
-  // iterates (mpcq::res_lanes(N) x 8 doubles, rho, 4 counters each), two dispatch lists and a
-  // status scratch (3 B int32), the device / pinned-host count of the next slice
+  // iterates (mpcq::res_lanes(N) x 8 doubles, rho, key, 4 counters each), the resumed launch's
+  // dispatch list (B int32, of 3 B: two once held alternating lists) and a status scratch, the
+  // device / pinned-host count of the resumed launch
   int32_t slice_iters = 0;
   double* res = nullptr;
   double* res_rho = nullptr;
@@ -520,9 +521,10 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
     a.order = order;
   }
   // sliced (mpcq_set_slice, beyond 16 stages): the first launch suspends every instance still
-  // running after slice_iters iterations; each further launch resumes the suspended ones, the
-  // farthest from convergence (primal residual / tolerance) first, for another slice, until none
-  // is left (a count read back per slice)
+  // running after slice_iters iterations; a second launch resumes the suspended ones, the
+  // farthest from convergence (primal residual / tolerance) first, and runs them to their end
+  // (the count read back in between).  (Re-slicing the second launch too was slower: C3 39.0 k
+  // against 44.1 k QP/s at 1200, profiles/r06r_*.)
   const bool sliced = c->slice_iters > 0 && c->slice_iters < c->p.max_iter && (N > 16 || getenv("MPCQ_SLICE16"));
   if (sliced) {
     rc = ensure_slice(c, B);
@@ -536,25 +538,19 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
   }
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   HIP_TRY(mpcq::launch_solve(N, fused, c->p, a, c->stream));
-  if (sliced) {
-    const int32_t* prev = a.order;
-    int64_t cnt = B;
-    const int max_slices = c->p.max_iter / c->slice_iters + 2;
-    for (int sl = 0;; ++sl) {
-      if (sl > max_slices) return fail(MPCQ_E_DEVICE, "sliced solve: instances still suspended after %d slices", sl);
-      int32_t* list = c->sl_buf + (sl & 1) * B;
-      HIP_TRY(mpcq::launch_suspended(prev, cnt, a.status, c->res_key, list, c->sl_count, c->stream));
-      HIP_TRY(hipMemcpyAsync(c->sl_host, c->sl_count, 4, hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      const int32_t left = *c->sl_host;
-      if (left <= 0) break;
+  if (sliced) {  // the suspended instances, farthest from convergence first, resumed once to their end
+    int32_t* list = c->sl_buf;
+    HIP_TRY(mpcq::launch_suspended(a.order, B, a.status, c->res_key, list, c->sl_count, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->sl_host, c->sl_count, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const int32_t left = *c->sl_host;
+    if (left > 0) {
       mpcq::LaunchArgs r = a;
       r.batch = left;
       r.order = list;
       r.resume = 1;
+      r.slice_iters = 0;
       HIP_TRY(mpcq::launch_solve(N, fused, c->p, r, c->stream));
-      prev = list;
-      cnt = left;
     }
   }
   HIP_TRY(hipEventRecord(c->ev[3], c->stream));

@@ -204,9 +204,10 @@ class Engine:
         self._call("mpcq_set_stream", self._h, C.c_void_p(stream_handle or 0))
 
     def set_slice(self, slice_iters: int):
-        """Sliced batch solves (mpcq_set_slice): beyond 16 stages each batch solve runs as
-        launches of up to ``slice_iters`` ADMM iterations per instance, the suspended ones
-        resumed until none is left -- bit-identical outputs, a shorter dispatch tail.  0: off."""
+        """Sliced batch solves (mpcq_set_slice): beyond 16 stages each batch solve suspends the
+        instances still iterating after ``slice_iters`` ADMM iterations and resumes them in a
+        second launch, the farthest from convergence first, to their end -- bit-identical
+        outputs, a shorter dispatch tail.  0: off."""
         self._call("mpcq_set_slice", self._h, int(slice_iters))
 
     def solve_device(self, batch: int, xref_ptr: int, fsteps_ptr: int, f0_ptr: int, status_ptr: int,

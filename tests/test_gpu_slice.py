@@ -2,8 +2,9 @@
 
 Beyond 16 stages a sliced solve suspends every instance still iterating at the first ADMM
 segment end after `slice` iterations, saves its iterate (x, z, y of every lane, rho, the loop
-counters) and resumes the suspended instances in further launches -- the formulation, the
-scaling and the factorisation at the saved rho recomputed, which gives the same bits.  Every
+counters) and resumes the suspended instances in a second launch, the farthest from convergence
+first, to their end -- the formulation, the scaling and the factorisation at the saved rho
+recomputed, which gives the same bits.  Every
 output must be bit-identical to the unsliced solve's: forces, x, y, statuses, iteration counts,
 rho, rho updates, the ADMM status (and polish's outcome in the polish = 2 instantiation).
 Slice lengths below, at and off the check interval (25), warm starts, the class order, the QP

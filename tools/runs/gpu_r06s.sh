@@ -1,0 +1,11 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+# r06s: sliced solves resumed once, to the end (the API's semantics now; r06r's MPCQ_SLICE_ONCE
+# experiment) -- the slicing tests, then C3 at slices of 900 / 1000 / 1100 / 1200 / 1300 / 1400
+O=gpurun_out
+T=r06s
+L="--companion 0 --reference25 0 --cpu-sample 0 --certify 0 --restatement 1024"
+timeout -k 10 400 python -u -m pytest tests/test_gpu_slice.py -x -v --timeout 240 --timeout-method thread > $O/${T}_pytest_slice.log 2>&1 || exit 1
+for q in 900 1000 1100 1200 1300 1400; do
+  timeout -k 10 240 python -u bench.py --config c3 $L --slice $q > $O/${T}_bench_c3_s$q.json 2> $O/${T}_bench_c3_s$q.err || exit 1
+done

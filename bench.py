@@ -121,7 +121,7 @@ def parse():
     return ap.parse_args()
 
 
-AUTO_SLICE = 1600  # bench.py --slice -1 beyond 16 stages
+AUTO_SLICE = 1200  # bench.py --slice -1 beyond 16 stages (C3: r06r / r06s)
 
 
 def load_pmc(tag: str, src_sha: str | None = None, path: str | None = None) -> dict:

@@ -1,12 +1,12 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-# r06p: the round's final build (sliced solves beyond 16 stages, bench.py slicing C3 at 1600 by
+# r06t: the round's final build (sliced solves beyond 16 stages, resumed once residual-first; bench.py slicing C3 at 1200 by
 # default) -- smoke, the whole GPU suite, per-iteration times, then every configuration profiled
 # (tools/profile.sh, summarised on the box into profiles/pmc_traffic.json) before its bench line:
 # C2, C3 (sliced: figures per solve), the C4 / C5 rank shards, whole C4 / C5 on one GPU; C1, the
 # session tick, the planner, the 2-rank gloo rehearsal
 O=gpurun_out
-T=r06p
+T=r06t
 prof() {  # tag key instances bench-args...
   local tag=$1 key=$2 n=$3; shift 3
   bash tools/profile.sh $tag "$@" && python3 tools/prof_summary.py $tag --key $key --instances $n > $O/${tag}_summary.txt 2>&1
@@ -16,7 +16,7 @@ timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout
 timeout -k 10 240 python -u tools/iterbench.py --N 16 --batches 256 > $O/${T}_iter16.txt 2>&1 &&
 timeout -k 10 240 python -u tools/iterbench.py --N 32 --batches 256 > $O/${T}_iter32.txt 2>&1 &&
 prof ${T} c2_N16_B1024 1024 --config c2 &&
-prof ${T}c3 c3_N32_B1024_s1600 1024 --config c3 &&
+prof ${T}c3 c3_N32_B1024_s1200 1024 --config c3 &&
 prof ${T}c4s c4_N16_B8192 8192 --config c4 --batch 8192 &&
 prof ${T}c5s c5_N16_B4096 4096 --config c5 --batch 4096 &&
 timeout -k 10 300 python -u bench.py > $O/${T}_bench_c2.json 2> $O/${T}_bench_c2.err &&

@@ -80,10 +80,13 @@ def test_slices_qp_entry_point():
         _same(ref, e1.qp_solve(qp["Ax"], qp["l"], qp["u"]), "qp")
 
 
-def test_slices_beyond_32_stages():
+@pytest.mark.parametrize("N", [48, 64])
+def test_slices_beyond_32_stages(N):
+    """The global-workspace layouts: S^-1 / R^-1 Q in the workspace (N > 32), the F_k rows and
+    the scaled constraint values too (N > 48 / 49), whose recomputation the resume relies on."""
     from mpcq import synth
-    syn = synth.make_batch(48, 48, gaits=("trot",), seed=3)
-    _pair(48, syn, (150,))
+    syn = synth.make_batch(48 if N == 48 else 24, N, gaits=("trot",), seed=3)
+    _pair(N, syn, (150,))
 
 
 def test_slice_is_a_no_op_at_16_stages():

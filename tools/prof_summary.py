@@ -59,9 +59,11 @@ def main():
     ap.add_argument("--key", default="c2_N16_B1024")
     ap.add_argument("--instances", type=int, default=1024)
     ap.add_argument("--kernel", default="engine_kernel", help="substring of the kernel the counters describe")
+    ap.add_argument("--src-dir", default=None, help="the profile.sh output (default gpurun_out/prof_<tag>)")
+    ap.add_argument("--out-dir", default=None, help="where the summary and pmc_traffic.json go (default profiles/)")
     a = ap.parse_args()
-    src = os.path.join(REPO, "gpurun_out", f"prof_{a.tag}")
-    dst = os.path.join(REPO, "profiles")
+    src = a.src_dir or os.path.join(REPO, "gpurun_out", f"prof_{a.tag}")
+    dst = a.out_dir or os.path.join(REPO, "profiles")
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{a.tag}_kernel_stats.csv"))
 
@@ -124,7 +126,7 @@ def main():
                      f"{t['SGPR_Count']}) are the dispatch's allocation fields, not the compiler's count (below)")
     # the compiler's own budget for the profiled horizon (tools/resource_usage.py)
     try:
-        ru = json.load(open(os.path.join(REPO, "profiles", "resource_usage.json")))
+        ru = json.load(open(os.path.join(REPO, "profiles", "resource_usage.json")))  # (the committed one)
         N = a.key.split("_N")[1].split("_")[0] if "_N" in a.key else None
         for kind, v in (ru.get(N) or {}).items():
             if kind.startswith("fused solve"):

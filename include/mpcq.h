@@ -161,9 +161,9 @@ int mpcq_last_kernel_ms(mpcq_ctx* ctx, double* formulate_ms, double* solve_ms);
  * convergence (primal residual over its tolerance) first, and runs them to their end.  Every
  * output is bit-identical to the unsliced solve's; long instances no longer hold a CU slot
  * past the others and start first once known, so a batch whose instances fill the CUs in
- * several rounds ends sooner.  The host reads one count back between
- * the launches (the call synchronises ctx's stream there).  0 (the default), a slice of
- * max_iter or more, and horizons up to 16: one launch. */
+ * several rounds ends sooner.  No host synchronisation: the second
+ * launch reads its workgroup count on the device (MPCQ_FLAG_ASYNC holds).  0 (the default), a
+ * slice of max_iter or more, and horizons up to 16: one launch. */
 int mpcq_set_slice(mpcq_ctx* ctx, int32_t slice_iters);
 
 /* ---- formulation -----------------------------------------------------------

@@ -37,7 +37,7 @@ struct mpcq_ctx {
   // sliced solves (mpcq_set_slice): the slice length (0: off), the suspended instances'
   // iterates (mpcq::res_lanes(N) x 8 doubles, rho, key, 4 counters each), the resumed launch's
   // dispatch list (B int32, of 3 B: two once held alternating lists) and a status scratch, the
-  // device / pinned-host count of the resumed launch
+  // resumed launch's workgroup count (device)
   int32_t slice_iters = 0;
   double* res = nullptr;
   double* res_rho = nullptr;
@@ -46,7 +46,6 @@ struct mpcq_ctx {
   int32_t* sl_buf = nullptr;
   int64_t sl_cap = 0;
   int32_t* sl_count = nullptr;
-  int32_t* sl_host = nullptr;
 };
 
 namespace {
@@ -219,10 +218,6 @@ int ensure_slice(mpcq_ctx* c, int64_t B) {
       c->sl_count = nullptr;
       return fail(MPCQ_E_NOMEM, "hipMalloc(4) for the slice count failed");
     }
-    if (hipHostMalloc(&c->sl_host, 4, hipHostMallocDefault) != hipSuccess) {
-      c->sl_host = nullptr;
-      return fail(MPCQ_E_NOMEM, "hipHostMalloc(4) for the slice count failed");
-    }
   }
   if (B > c->sl_cap) {
     if (c->res) {
@@ -385,7 +380,6 @@ int mpcq_destroy(mpcq_ctx* c) {
   if (c->res) (void)hipFree(c->res);
   if (c->sl_buf) (void)hipFree(c->sl_buf);
   if (c->sl_count) (void)hipFree(c->sl_count);
-  if (c->sl_host) (void)hipHostFree(c->sl_host);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -522,8 +516,7 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
   }
   // sliced (mpcq_set_slice, beyond 16 stages): the first launch suspends every instance still
   // running after slice_iters iterations; a second launch resumes the suspended ones, the
-  // farthest from convergence (primal residual / tolerance) first, and runs them to their end
-  // (the count read back in between).  (Re-slicing the second launch too was slower: C3 39.0 k
+  // farthest from convergence (primal residual / tolerance) first, and runs them to their end.  (Re-slicing the second launch too was slower: C3 39.0 k
   // against 44.1 k QP/s at 1200, profiles/r06r_*.)
   const bool sliced = c->slice_iters > 0 && c->slice_iters < c->p.max_iter && (N > 16 || getenv("MPCQ_SLICE16"));
   if (sliced) {
@@ -539,19 +532,16 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   HIP_TRY(mpcq::launch_solve(N, fused, c->p, a, c->stream));
   if (sliced) {  // the suspended instances, farthest from convergence first, resumed once to their end
+    // (the resumed launch is sized for the whole batch and reads the count from the device:
+    // workgroups past it return at once -- no host round trip, the call stays asynchronous)
     int32_t* list = c->sl_buf;
     HIP_TRY(mpcq::launch_suspended(a.order, B, a.status, c->res_key, list, c->sl_count, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->sl_host, c->sl_count, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    const int32_t left = *c->sl_host;
-    if (left > 0) {
-      mpcq::LaunchArgs r = a;
-      r.batch = left;
-      r.order = list;
-      r.resume = 1;
-      r.slice_iters = 0;
-      HIP_TRY(mpcq::launch_solve(N, fused, c->p, r, c->stream));
-    }
+    mpcq::LaunchArgs r = a;
+    r.order = list;
+    r.batch_dev = c->sl_count;
+    r.resume = 1;
+    r.slice_iters = 0;
+    HIP_TRY(mpcq::launch_solve(N, fused, c->p, r, c->stream));
   }
   HIP_TRY(hipEventRecord(c->ev[3], c->stream));
   if (by_class) HIP_TRY(mpcq::launch_class_learn(cls, its, B, c->cls_sum, c->cls_cnt, c->stream));

@@ -932,6 +932,9 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
   int cc = cl ? c : 2;            // column component; c == 3 shadows c == 2
   int ph = 3 * f + cc;            // own force / state index in the stage
   if ((int64_t)blockIdx.x >= a.batch) return;
+  if constexpr (kSlice<N>) {  // (a resumed slice: its count is on the device, no host round trip)
+    if (a.batch_dev && (int64_t)blockIdx.x >= (int64_t)*a.batch_dev) return;
+  }
   const int64_t b = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;  // the instance
   STAMP_DECL
   constexpr bool BIG = kBig<N>, ABG = kAbG<N>;

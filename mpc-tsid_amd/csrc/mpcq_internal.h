@@ -41,6 +41,8 @@ struct LaunchArgs {
   // the same bits) instead of the cold point.
   int32_t slice_iters;
   int32_t resume;
+  const int32_t* batch_dev;  // (the resumed launch) the count of workgroups with work, on the device:
+                             // the launch is sized for the whole batch, workgroups past it return
   double* res;          // [B][8][res_lanes(N)]: xf, xX, z[3], y[3] of every lane
   double* res_rho;      // [B]
   double* res_key;      // [B]: the primal residual over its tolerance at suspension (the next

@@ -79,14 +79,14 @@ def main():
         if k2 != "SQ_WAVES":
             sq[k2] = v2
     f64 = counters(os.path.join(src, "f64", "run_counter_collection.csv"), a.kernel)
-    # figures per solve: a sliced solve (mpcq_set_slice) is its first launch (the whole batch's
-    # grid) and the resumed launches after it (smaller grids); unsliced, a solve is one launch.
-    # The counter passes replay the same launches: their kernel time is the trace's.
+    # figures per solve: a sliced solve (mpcq_set_slice) is two engine launches around one
+    # suspended_kernel (the compaction), both sized for the whole batch; unsliced, a solve is one
+    # launch.  The counter passes replay the same launches: their kernel time is the trace's.
     grids = [int(r["Grid_Size_X"]) for r in trace]
-    solves = sum(1 for g in grids if g == max(grids)) if grids else 0
-    dispatches = len(trace)
-    if not solves:
-        solves = max(1, sum(int(r["Calls"]) for r in eng))
+    dispatches = len(trace) or sum(int(r["Calls"]) for r in eng)
+    compactions = sum(int(r["Calls"]) for r in others if "suspended_kernel" in r["Name"])
+    solves = compactions if compactions else dispatches
+    solves = max(1, solves)
     kern_ms = (sum(float(r["AverageNs"]) * int(r["Calls"]) for r in eng) / solves / 1e6) if eng else None
 
     def mean(v):  # (per solve: the sum over its launches; one launch each when unsliced)
@@ -108,9 +108,9 @@ def main():
     lines = [f"# rocprofv3 summary `{a.tag}` ({a.key})", "",
              f"- build: libmpcq.so engine_src_sha `{sha}` (mpcq_build_info of the profiled process, every pass)"]
     if dispatches > solves:
-        lines.append(f"- sliced solves: {dispatches} engine launches for {solves} solves (the first slice's grid "
-                     f"{max(grids)} threads, the resumed slices' smaller); the kernel time, counters and traffic below "
-                     f"are per solve (the sum over its slices): {kern_ms:.3f} ms")
+        lines.append(f"- sliced solves: {dispatches} engine launches for {solves} solves (one compaction each); the "
+                     f"kernel time, counters and traffic below are per solve (the sum over its launches): "
+                     f"{kern_ms:.3f} ms")
     for r in eng:
         lines.append(f"- kernel `{r['Name']}`: {r['Calls']} calls, average {float(r['AverageNs']) / 1e6:.3f} ms "
                      f"(min {float(r['MinNs']) / 1e6:.3f}, max {float(r['MaxNs']) / 1e6:.3f}), "
@@ -139,10 +139,11 @@ def main():
     if fk is not None and wk is not None:
         rd_raw, wr = fk * 1024, wk * 1024
         traffic = 2 * rd_raw + wr
-        lines += ["", "## HBM counters (per launch)", "",
+        lines += ["", "## HBM counters (per solve)" if dispatches > solves else "## HBM counters (per launch)", "",
                   f"- FETCH_SIZE {fk:.1f} KiB -> {rd_raw / 1e6:.3f} MB raw, {2 * rd_raw / 1e6:.3f} MB with the gfx950 x2 correction",
                   f"- WRITE_SIZE {wk:.1f} KiB -> {wr / 1e6:.3f} MB",
-                  f"- traffic (corrected read + write) {traffic / 1e6:.3f} MB per launch = {traffic / a.instances:.0f} B per instance"]
+                  f"- traffic (corrected read + write) {traffic / 1e6:.3f} MB per {'solve' if dispatches > solves else 'launch'} "
+                  f"= {traffic / a.instances:.0f} B per instance"]
     if sq:
         w = mean(sq.get("SQ_WAVES", [])) or 1.0
         cyc = mean(sq.get("SQ_WAVE_CYCLES", [])) or 0.0

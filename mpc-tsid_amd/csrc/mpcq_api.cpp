@@ -228,7 +228,7 @@ int ensure_slice(mpcq_ctx* c, int64_t B) {
     c->res = nullptr;
     c->sl_buf = nullptr;
     c->sl_cap = 0;
-    const size_t rb = (size_t)B * (8 * (size_t)mpcq::res_lanes(c->N) + 2) * 8 + (size_t)B * 16;
+    const size_t rb = (size_t)B * (8 * (size_t)mpcq::res_lanes(c->N) + 3) * 8 + (size_t)B * 32;
     if (hipMalloc(&c->res, rb) != hipSuccess) {
       c->res = nullptr;
       return fail(MPCQ_E_NOMEM, "hipMalloc(%zu) for the suspended iterates failed", rb);
@@ -239,7 +239,7 @@ int ensure_slice(mpcq_ctx* c, int64_t B) {
     }
     c->res_rho = c->res + (size_t)B * 8 * (size_t)mpcq::res_lanes(c->N);
     c->res_key = c->res_rho + B;
-    c->res_i = (int32_t*)(c->res_key + B);
+    c->res_i = (int32_t*)(c->res_key + 2 * B);
     c->sl_cap = B;
   }
   return MPCQ_OK;

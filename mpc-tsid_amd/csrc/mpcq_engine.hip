@@ -1196,7 +1196,7 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
     // (a resumed slice: the rho and the update count it was suspended with)
     double rho_s = kSlice<N> && a.resume ? a.res_rho[b] : (a.rho_in ? a.rho_in[b] : p.rho);
     rho_s = fmin(fmax(rho_s, kRhoMin), kRhoMax);
-    if (kSlice<N> && a.resume) n_upd = a.res_i[4 * b + 3];
+    if (kSlice<N> && a.resume) n_upd = a.res_i[8 * b + 3];
 
     // per-row rho / 1/rho from the row's class and the (uniform) rho values
     double r_in = 0.0, r_eq = 0.0, ri_in = 0.0, ri_eq = 0.0;
@@ -3473,9 +3473,9 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
       // a resumed slice continues the saved loop counters; slice_iters > 0 suspends at the
       // first segment end slice_iters iterations on (mpcq_set_slice)
       if (kSlice<N> && a.resume) {
-        iter = __builtin_amdgcn_readfirstlane(a.res_i[4 * b]);
-        to_check = __builtin_amdgcn_readfirstlane(a.res_i[4 * b + 1]);
-        to_adapt = __builtin_amdgcn_readfirstlane(a.res_i[4 * b + 2]);
+        iter = __builtin_amdgcn_readfirstlane(a.res_i[8 * b]);
+        to_check = __builtin_amdgcn_readfirstlane(a.res_i[8 * b + 1]);
+        to_adapt = __builtin_amdgcn_readfirstlane(a.res_i[8 * b + 2]);
       }
       const int slice_end =
           kSlice<N> && a.slice_iters > 0 && a.slice_iters < p.max_iter ? iter + a.slice_iters : 0x7fffffff;
@@ -3601,6 +3601,13 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
           }
           STAMP(11);
           ++iter;
+          // (a sliced launch) the residuals over their tolerances at the last segment end up to
+          // half way through the slice, for the suspended instance's key (below)
+          if (kSlice<N> && a.slice_iters > 0 && iter <= slice_end - (a.slice_iters >> 1) && t == 0) {
+            a.res_key[2 * b] = pri_res / eps_pri;
+            a.res_key[2 * b + 1] = dua_res / eps_dua;
+            a.res_i[8 * b + 4] = iter;
+          }
           if (kSlice<N> && iter >= slice_end && iter <= p.max_iter) {  // (uniform) suspend this slice here
             suspended = true;
             break;
@@ -3617,11 +3624,21 @@ void engine_kernel(mpcq_params p, LaunchArgs a) {
         for (int j = 0; j < 3; ++j) { q[(2 + j) * RL] = z[j]; q[(5 + j) * RL] = y[j]; }
         if (t == 0) {
           a.res_rho[b] = rho_s;
-          a.res_key[b] = pri_res / eps_pri;  // (the last segment end's update_info)
-          a.res_i[4 * b] = iter;
-          a.res_i[4 * b + 1] = to_check;
-          a.res_i[4 * b + 2] = to_adapt;
-          a.res_i[4 * b + 3] = n_upd;
+          // the key: the iterations left, extrapolated from the residuals' geometric decay between
+          // the half-way sample and now, primal and dual, the larger (a residual not decaying, or
+          // no half-way sample: as long as can be); 0 for one already within its tolerance
+          const int i1 = a.res_i[8 * b + 4];
+          const double rp = pri_res / eps_pri, rd = dua_res / eps_dua;
+          auto left = [&](double r1, double r2) __attribute__((always_inline)) -> double {
+            if (!(r2 > 1.0)) return 0.0;
+            if (i1 <= 0 || !(r1 > r2)) return 1e30;
+            return log(r2) / log(r1 / r2) * (double)(iter - i1);
+          };
+          a.res_key[2 * b] = fmax(left(a.res_key[2 * b], rp), left(a.res_key[2 * b + 1], rd));
+          a.res_i[8 * b] = iter;
+          a.res_i[8 * b + 1] = to_check;
+          a.res_i[8 * b + 2] = to_adapt;
+          a.res_i[8 * b + 3] = n_upd;
           if (a.status) a.status[b] = kStatusSuspended;
         }
         return;

@@ -45,9 +45,11 @@ struct LaunchArgs {
                              // the launch is sized for the whole batch, workgroups past it return
   double* res;          // [B][8][res_lanes(N)]: xf, xX, z[3], y[3] of every lane
   double* res_rho;      // [B]
-  double* res_key;      // [B]: the primal residual over its tolerance at suspension (the next
-                        // slice's order: Spearman +0.98 with the final count on C3)
-  int32_t* res_i;       // [B][4]: next iteration, to the next check, to the next adaptation, rho updates
+  double* res_key;      // [B][2]: the primal / dual residual over its tolerance half way through the
+                        // slice, then (at suspension) [b][0] = the iterations left, extrapolated from
+                        // their decay since -- the resumed launch's order
+  int32_t* res_i;       // [B][8]: next iteration, to the next check, to the next adaptation, rho
+                        // updates, the half-way sample's iteration, 3 spare
 };
 constexpr int32_t kStatusSuspended = 100;  // (internal: the host loop resumes these)
 constexpr int64_t res_lanes(int N) { return 16 * (int64_t)((N + 3) & ~3); }
@@ -149,8 +151,8 @@ hipError_t launch_class_order(const double* fsteps, int64_t batch, int32_t* cls,
 hipError_t launch_class_learn(const int32_t* cls, const int32_t* iters, int64_t batch, uint64_t* sum,
                               uint32_t* cnt, hipStream_t s);
 // Sliced solves: list[*count] = the instances of prev[0..n) (null: 0..n-1) whose status is
-// kStatusSuspended, the largest key (res_key: primal residual / tolerance) first, in prev's
-// order inside a key bucket (one workgroup; buckets of 1/8 octave).
+// kStatusSuspended, the largest key (key[2 id]: the iterations left, extrapolated) first, in
+// prev's order inside a key bucket (one workgroup; buckets of 1/8 octave).
 hipError_t launch_suspended(const int32_t* prev, int64_t n, const int32_t* status, const double* key,
                             int32_t* list, int32_t* count, hipStream_t s);
 

@@ -161,10 +161,11 @@ __global__ __launch_bounds__(256) void class_learn_kernel(const int32_t* __restr
 }
 
 // Sliced solves (mpcq_set_slice): the suspended instances of the last launch for the next one,
-// the largest key first -- the primal residual over its tolerance when the instance was
-// suspended, which ranks the remaining work (Spearman +0.98 with the final iteration count over
-// C3's instances suspended at 1600 iterations) -- in buckets of 1/8 octave, the last launch's
-// order inside a bucket: a stable counting sort in one workgroup (the class order's scheme)
+// the largest key first -- the iterations left, extrapolated from the residuals' decay over the
+// second half of the slice (Spearman +0.995 with the final iteration count over C3's instances
+// suspended at 1200 iterations, tools/resume_predictors.py) -- in buckets of 1/8 octave, the last
+// launch's order inside a bucket: a stable counting sort in one workgroup (the class order's
+// scheme)
 __device__ __forceinline__ int key_bucket(double v) {
   if (!(v > 0.0)) return 0;
   const double e = floor(8.0 * log2(v)) + 128.0;  // (1/8 octave; keys from 2^-16 to 2^16)
@@ -183,7 +184,7 @@ __global__ __launch_bounds__(1024) void suspended_kernel(const int32_t* __restri
   __syncthreads();
   for (int64_t i = t; i < n; i += blockDim.x) {
     const int32_t id = prev ? prev[i] : (int32_t)i;
-    if (status[id] == kStatusSuspended) atomicAdd(&base[key_bucket(key[id])], 1);
+    if (status[id] == kStatusSuspended) atomicAdd(&base[key_bucket(key[2 * id])], 1);
   }
   __syncthreads();
   if (w == 0) {  // exclusive offsets, the largest key first (four buckets per lane)
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(1024) void suspended_kernel(const int32_t* __restri
     int q = -1;
     if (i < n) {
       id = prev ? prev[i] : (int32_t)i;
-      if (status[id] == kStatusSuspended) q = key_bucket(key[id]);
+      if (status[id] == kStatusSuspended) q = key_bucket(key[2 * id]);
     }
     int rank = 0;
     bool done = q < 0;

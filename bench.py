@@ -121,7 +121,7 @@ def parse():
     return ap.parse_args()
 
 
-AUTO_SLICE = 1200  # bench.py --slice -1 beyond 16 stages (C3: r06r / r06s)
+AUTO_SLICE = 1000  # bench.py --slice -1 beyond 16 stages (C3: r06y / r06z)
 
 
 def load_pmc(tag: str, src_sha: str | None = None, path: str | None = None) -> dict:

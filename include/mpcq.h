@@ -158,8 +158,8 @@ int mpcq_last_kernel_ms(mpcq_ctx* ctx, double* formulate_ms, double* solve_ms);
  * at the first ADMM segment end (check / adaptive-rho / max_iter boundary) after slice_iters
  * iterations and saves its iterate in device scratch; the second resumes the suspended ones
  * (formulation, scaling and the factorisation at the saved rho recomputed), the farthest from
- * convergence (primal residual over its tolerance) first, and runs them to their end.  Every
- * output is bit-identical to the unsliced solve's; long instances no longer hold a CU slot
+ * convergence (the iterations left, extrapolated from the residuals' decay) first, to their
+ * end.  Every output is bit-identical to the unsliced solve's; long instances no longer hold a CU slot
  * past the others and start first once known, so a batch whose instances fill the CUs in
  * several rounds ends sooner.  No host synchronisation: the second
  * launch reads its workgroup count on the device (MPCQ_FLAG_ASYNC holds).  0 (the default), a

@@ -516,7 +516,8 @@ static int solve_common(mpcq_ctx* c, int64_t B, bool fused, const double* xref, 
   }
   // sliced (mpcq_set_slice, beyond 16 stages): the first launch suspends every instance still
   // running after slice_iters iterations; a second launch resumes the suspended ones, the
-  // farthest from convergence (primal residual / tolerance) first, and runs them to their end.  (Re-slicing the second launch too was slower: C3 39.0 k
+  // farthest from convergence (the iterations left, extrapolated from the residuals' decay)
+  // first, and runs them to their end.  (Re-slicing the second launch too was slower: C3 39.0 k
   // against 44.1 k QP/s at 1200, profiles/r06r_*.)
   const bool sliced = c->slice_iters > 0 && c->slice_iters < c->p.max_iter && (N > 16 || getenv("MPCQ_SLICE16"));
   if (sliced) {
